@@ -1,0 +1,52 @@
+"""Bootstrap of the solver's RCCL communicator from torch.distributed.
+
+One process per GPU (torchrun / torch.distributed.run).  The solver owns its own RCCL
+communicator (created in C++ with ncclCommInitRank) so its all-to-alls can be enqueued on its own
+streams and captured in its hipGraph; torch.distributed is only used to agree on the 128-byte
+ncclUniqueId (rank 0 creates it, broadcast_object_list distributes it) and for host-side barriers
+and timing reductions.  The reference bootstrapped nothing: it used host MPI for all data
+movement (channel_cuda_mpi.c:64-128) and bound rank%2 to a device (main.c:87).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from .._native import require_native
+
+
+def dist_info() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from torch.distributed or the torchrun environment."""
+    if dist.is_available() and dist.is_initialized():
+        rank, world = dist.get_rank(), dist.get_world_size()
+    else:
+        rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    return rank, world, local
+
+
+def nccl_unique_id() -> bytes:
+    """Create the RCCL unique id on rank 0 and share it with every rank (empty for 1 rank)."""
+    rank, world, _ = dist_info()
+    if world == 1:
+        return b""
+    if not dist.is_initialized():
+        raise RuntimeError("world_size > 1 requires torch.distributed to be initialised")
+    obj = [require_native().new_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from the torchrun environment if needed; set the device."""
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        dist.init_process_group(backend=backend)
+    rank, world, local = dist_info()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    return rank, world, local

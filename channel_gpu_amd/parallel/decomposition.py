@@ -1,0 +1,61 @@
+"""Slab decomposition math (Python mirror of csrc/core/plan.cpp, used by tests and tools).
+
+Spectral state per rank: [y (all NY)][kx_local][kz]; physical per rank: [y_local][x][kz].
+Every split is balanced (counts differ by at most one), so NY = 385 at P = 8 works — the
+reference required NX == NY, NY % P == 0 and NX/P % 64 == 0.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+
+def balanced_split(n: int, parts: int) -> tuple[list[int], list[int]]:
+    if parts < 1 or n < parts:
+        raise ValueError(f"cannot split {n} items over {parts} parts")
+    base, rem = divmod(n, parts)
+    count = [base + (1 if p < rem else 0) for p in range(parts)]
+    start, off = [], 0
+    for c in count:
+        start.append(off)
+        off += c
+    return start, count
+
+
+@dataclasses.dataclass(frozen=True)
+class SlabDecomposition:
+    NX: int
+    NY: int
+    NZ: int
+    P: int
+
+    @property
+    def Kx(self) -> int:
+        return self.NX // 3
+
+    @property
+    def nkx(self) -> int:
+        return 2 * self.Kx + 1
+
+    @property
+    def nkz(self) -> int:
+        return (2 * self.NZ - 2) // 3 + 1
+
+    def kx_split(self):
+        return balanced_split(self.nkx, self.P)
+
+    def y_split(self):
+        return balanced_split(self.NY, self.P)
+
+    def a2a_backward_bytes(self, rank: int, esz: int = 8) -> list[int]:
+        """bytes rank sends to each peer in one backward (spectral -> physical) all-to-all."""
+        ks, kc = self.kx_split()
+        ys, yc = self.y_split()
+        return [yc[q] * kc[rank] * self.nkz * esz for q in range(self.P)]
+
+    def a2a_off_rank_bytes_per_step(self, esz: int = 8) -> int:
+        """off-rank bytes per RK3 step for the busiest rank (6 backward + 3 forward per substep)."""
+        worst = 0
+        for r in range(self.P):
+            b = sum(x for q, x in enumerate(self.a2a_backward_bytes(r, esz)) if q != r)
+            worst = max(worst, b)
+        return 3 * 9 * worst

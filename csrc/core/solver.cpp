@@ -1,0 +1,810 @@
+#include "channel/solver.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+
+#include "channel/common.hpp"
+#include "channel/io.hpp"
+
+namespace channel {
+
+namespace {
+bool g_debug_sync = false;
+
+template <typename T2>
+void to_dev_type(const std::complex<double>* src, size_t n, std::vector<T2>& dst) {
+  dst.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    dst[i].x = static_cast<decltype(dst[i].x)>(src[i].real());
+    dst[i].y = static_cast<decltype(dst[i].x)>(src[i].imag());
+  }
+}
+
+// deterministic uniform [-1, 1) from a 64-bit key (splitmix64)
+double urand(unsigned long long key) {
+  unsigned long long z = key + 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z = z ^ (z >> 31);
+  return (static_cast<double>(z >> 11) / 9007199254740992.0) * 2.0 - 1.0;
+}
+
+// Thomas for complex RHS with real tridiagonal matrix (host, IC construction)
+void thomas(const std::vector<double>& a, const std::vector<double>& b, const std::vector<double>& c,
+            std::vector<std::complex<double>>& d) {
+  const int n = static_cast<int>(d.size());
+  std::vector<double> cp(n);
+  std::vector<std::complex<double>> dp(n);
+  cp[0] = c[0] / b[0];
+  dp[0] = d[0] / b[0];
+  for (int i = 1; i < n; ++i) {
+    const double m = b[i] - a[i] * cp[i - 1];
+    cp[i] = c[i] / m;
+    dp[i] = (d[i] - a[i] * dp[i - 1]) / m;
+  }
+  d[n - 1] = dp[n - 1];
+  for (int i = n - 2; i >= 0; --i) d[i] = dp[i] - cp[i] * d[i + 1];
+}
+}  // namespace
+
+bool debug_sync_enabled() { return g_debug_sync; }
+void set_debug_sync(bool on) { g_debug_sync = on; }
+
+Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::string& nccl_uid)
+    : cfg_(cfg), plan_(Plan::make(cfg, nranks, rank)), grid_(YGrid::build(cfg.NY, cfg.stretch)), device_(device) {
+  fp64_ = cfg_.fp64();
+  esz_ = fp64_ ? 16 : 8;
+  HIP_CHECK(hipSetDevice(device_));
+  HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
+  if (nranks > 1) {
+    CH_CHECK(!nccl_uid.empty(), "P > 1 requires an RCCL unique id");
+    comm_ = std::make_unique<Comm>(rank, nranks, nccl_uid, device_);
+    CH_CHECK(nranks <= 8, "slab decomposition supports P <= 8 ranks per job in this version");
+  }
+  ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
+  tw_x_.build(plan_.NX, fp64_);
+  tw_z_.build(plan_.Nzp, fp64_);
+  alloc();
+}
+
+Solver::~Solver() {
+  try {
+    if (s_comp_) (void)hipStreamSynchronize(s_comp_);
+    if (s_comm_) (void)hipStreamSynchronize(s_comm_);
+  } catch (...) {
+  }
+  free_all();
+  comm_.reset();
+  if (s_comp_) (void)hipStreamDestroy(s_comp_);
+  if (s_comm_) (void)hipStreamDestroy(s_comm_);
+}
+
+void Solver::alloc() {
+  const Plan& p = plan_;
+  spec_ = p.spec_elems();
+  physn_ = p.phys_elems();
+  xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz;
+  HIP_CHECK(hipMalloc(&state_, 4 * spec_ * esz_));
+  HIP_CHECK(hipMalloc(&out_, 6 * spec_ * esz_));
+  HIP_CHECK(hipMalloc(&phys_, std::max<size_t>(6 * physn_, 1) * esz_));
+  HIP_CHECK(hipMemset(state_, 0, 4 * spec_ * esz_));
+  HIP_CHECK(hipMemset(out_, 0, 6 * spec_ * esz_));
+  if (p.P > 1) {
+    HIP_CHECK(hipMalloc(&xbuf_, 6 * xstride_ * esz_));
+    HIP_CHECK(hipMemset(xbuf_, 0, 6 * xstride_ * esz_));
+  }
+  const int N = p.NY;
+  // scalars: dt, time, dtlog[8], stats[4N], mean[3N+8], invdy[N], maxima[4] (float), health
+  const size_t nd = 2 + 8 + 4 * N + (3 * N + 8) + N;
+  HIP_CHECK(hipMalloc(&dscal_, nd * sizeof(double) + 4 * sizeof(float) + 16));
+  HIP_CHECK(hipMemset(dscal_, 0, nd * sizeof(double) + 4 * sizeof(float) + 16));
+  double* d = static_cast<double*>(dscal_);
+  d_dt_ = d;
+  d_time_ = d + 1;
+  d_dtlog_ = d + 2;
+  d_stats_ = d + 10;
+  d_mean_ = d_stats_ + 4 * N;
+  d_invdy_ = d_mean_ + 3 * N + 8;
+  d_max_ = reinterpret_cast<float*>(d_invdy_ + N);
+  d_health_ = reinterpret_cast<unsigned*>(d_max_ + 4);
+  std::vector<double> invdy(N);
+  const auto& y = grid_.y;
+  for (int j = 0; j < N; ++j) {
+    const double h = (j == 0) ? y[1] - y[0] : (j == N - 1 ? y[N - 1] - y[N - 2] : 0.5 * (y[j + 1] - y[j - 1]));
+    invdy[j] = 1.0 / h;
+  }
+  HIP_CHECK(hipMemcpy(d_invdy_, invdy.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  ev_a2a_.resize(6);
+  ev_xf_.resize(3);
+  for (auto& e : ev_a2a_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : ev_xf_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_spec_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_phys_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_fwd_done_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_red_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_stats_, hipEventDisableTiming));
+  ph_ev_.resize(2 * 8);
+  for (auto& e : ph_ev_) HIP_CHECK(hipEventCreate(&e));
+  ph_ms_.assign(8, 0.0);
+}
+
+void Solver::free_all() {
+  for (int i = 0; i < 2; ++i)
+    if (gexec_[i]) (void)hipGraphExecDestroy(gexec_[i]);
+  for (auto e : ev_a2a_) (void)hipEventDestroy(e);
+  for (auto e : ev_xf_) (void)hipEventDestroy(e);
+  for (auto e : ph_ev_) (void)hipEventDestroy(e);
+  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
+    if (e) (void)hipEventDestroy(e);
+  for (void* p : {state_, out_, phys_, xbuf_, dscal_})
+    if (p) (void)hipFree(p);
+  state_ = out_ = phys_ = xbuf_ = dscal_ = nullptr;
+}
+
+void* Solver::field_ptr(int f) const {
+  char* st = static_cast<char*>(state_);
+  char* ou = static_cast<char*>(out_);
+  if (f >= PHI && f <= ROMEGA) return st + static_cast<size_t>(f) * spec_ * esz_;
+  if (f >= OUT0 && f <= OUT5) return ou + static_cast<size_t>(f - OUT0) * spec_ * esz_;
+  CH_CHECK(false, "bad field index " << f);
+}
+
+// ---- state ------------------------------------------------------------------------------------
+void Solver::set_state(const std::complex<double>* phi, const std::complex<double>* omega, const double* U) {
+  const Plan& p = plan_;
+  const int lines = p.lines_loc();
+  std::vector<std::complex<double>> om(omega, omega + spec_);
+  if (p.owns_mean()) {
+    for (int j = 0; j < p.NY; ++j) om[static_cast<size_t>(j) * lines] = std::complex<double>(U ? U[j] : 0.0, 0.0);
+  }
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  if (fp64_) {
+    std::vector<double2> h;
+    to_dev_type(phi, spec_, h);
+    HIP_CHECK(hipMemcpy(field_ptr(PHI), h.data(), spec_ * esz_, hipMemcpyHostToDevice));
+    to_dev_type(om.data(), spec_, h);
+    HIP_CHECK(hipMemcpy(field_ptr(OMEGA), h.data(), spec_ * esz_, hipMemcpyHostToDevice));
+  } else {
+    std::vector<float2> h;
+    to_dev_type(phi, spec_, h);
+    HIP_CHECK(hipMemcpy(field_ptr(PHI), h.data(), spec_ * esz_, hipMemcpyHostToDevice));
+    to_dev_type(om.data(), spec_, h);
+    HIP_CHECK(hipMemcpy(field_ptr(OMEGA), h.data(), spec_ * esz_, hipMemcpyHostToDevice));
+  }
+  HIP_CHECK(hipMemset(field_ptr(RPHI), 0, 2 * spec_ * esz_));
+  prepared_ = false;
+}
+
+void Solver::get_state(std::complex<double>* phi, std::complex<double>* omega, double* U) const {
+  const Plan& p = plan_;
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  auto fetch = [&](int f, std::complex<double>* dst) {
+    if (fp64_) {
+      std::vector<double2> h(spec_);
+      HIP_CHECK(hipMemcpy(h.data(), field_ptr(f), spec_ * esz_, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < spec_; ++i) dst[i] = {h[i].x, h[i].y};
+    } else {
+      std::vector<float2> h(spec_);
+      HIP_CHECK(hipMemcpy(h.data(), field_ptr(f), spec_ * esz_, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < spec_; ++i) dst[i] = {h[i].x, h[i].y};
+    }
+  };
+  fetch(PHI, phi);
+  fetch(OMEGA, omega);
+  const int lines = p.lines_loc();
+  for (int j = 0; j < p.NY; ++j) {
+    if (p.owns_mean()) {
+      if (U) U[j] = omega[static_cast<size_t>(j) * lines].real();
+      omega[static_cast<size_t>(j) * lines] = 0.0;
+    } else if (U) {
+      U[j] = 0.0;
+    }
+  }
+}
+
+void Solver::init_ic() {
+  const Plan& p = plan_;
+  const int N = p.NY, lines = p.lines_loc();
+  std::vector<std::complex<double>> phi(spec_), om(spec_);
+  std::vector<double> U(N);
+  const auto& y = grid_.y;
+  for (int j = 0; j < N; ++j) U[j] = (cfg_.ic == "zero") ? 0.0 : 0.75 * cfg_.Q * (1.0 - y[j] * y[j]);
+  if (cfg_.ic == "random") {
+    // full compact D2 with wall closure (reference secondDerivative, meanUevol.c:223-345)
+    std::vector<double> la(N, 0), lb(N, 1), lc(N, 0);
+    for (int j = 1; j < N - 1; ++j) { la[j] = grid_.m_lo[j]; lc[j] = grid_.m_up[j]; }
+    lc[0] = grid_.d2_w0_up;
+    la[N - 1] = grid_.d2_wN_lo;
+    std::vector<std::complex<double>> v(N), w(N);
+    const double amp = cfg_.ic_amplitude;
+    for (int ikx = 0; ikx < p.nkx_loc; ++ikx) {
+      const int ig = p.kx0 + ikx;
+      const int kx = p.kx_of(ig);
+      for (int kz = 0; kz < p.nkz; ++kz) {
+        const int line = ikx * p.nkz + kz;
+        if (kx == 0 && kz == 0) continue;
+        const double al = p.ax * kx, be = p.az * kz, k2 = al * al + be * be;
+        const double env = std::exp(-k2 / 32.0);
+        const bool cj = (kz == 0 && kx < 0);
+        const unsigned long long base =
+            (cfg_.seed * 1000003ULL + static_cast<unsigned long long>(std::abs(kx))) * 1000033ULL + kz;
+        for (int j = 0; j < N; ++j) {
+          const unsigned long long key = base * 4099ULL + j;
+          const double w1 = 1.0 - y[j] * y[j];
+          std::complex<double> vr(urand(key * 4 + 0), urand(key * 4 + 1));
+          std::complex<double> orr(urand(key * 4 + 2), urand(key * 4 + 3));
+          if (cj) { vr = std::conj(vr); orr = std::conj(orr); }
+          if (kz == 0 && kx == 0) { vr = vr.real(); orr = orr.real(); }
+          v[j] = amp * env * w1 * w1 * vr;
+          w[j] = amp * env * w1 * orr;
+        }
+        v[0] = v[N - 1] = 0.0;
+        w[0] = w[N - 1] = 0.0;
+        // phi = D2 v - k2 v
+        std::vector<std::complex<double>> d2(N);
+        d2[0] = grid_.d2_w0[0] * v[0] + grid_.d2_w0[1] * v[1] + grid_.d2_w0[2] * v[2];
+        d2[N - 1] = grid_.d2_wN[0] * v[N - 1] + grid_.d2_wN[1] * v[N - 2] + grid_.d2_wN[2] * v[N - 3];
+        for (int j = 1; j < N - 1; ++j) d2[j] = grid_.k_lo[j] * v[j - 1] + grid_.k_c[j] * v[j] + grid_.k_up[j] * v[j + 1];
+        thomas(la, lb, lc, d2);
+        for (int j = 0; j < N; ++j) {
+          phi[static_cast<size_t>(j) * lines + line] = d2[j] - k2 * v[j];
+          om[static_cast<size_t>(j) * lines + line] = w[j];
+        }
+      }
+    }
+  } else {
+    CH_CHECK(cfg_.ic == "laminar" || cfg_.ic == "zero", "init_ic: ic='" << cfg_.ic << "' needs set_state / read_restart");
+  }
+  set_state(phi.data(), om.data(), U.data());
+  double zero2[2] = {0.0, 0.0};
+  HIP_CHECK(hipMemcpy(d_dt_, zero2, 2 * sizeof(double), hipMemcpyHostToDevice));
+  nstep_ = 0;
+}
+
+void Solver::set_time(double t, double dt) {
+  double v[2] = {dt, t};
+  HIP_CHECK(hipMemcpy(d_dt_, v, 2 * sizeof(double), hipMemcpyHostToDevice));
+}
+
+double Solver::time() const {
+  double t = 0;
+  HIP_CHECK(hipMemcpy(&t, d_time_, sizeof(double), hipMemcpyDeviceToHost));
+  return t;
+}
+
+// ---- pipeline ----------------------------------------------------------------------------------
+void Solver::kspec(int mode, int n, bool stats) {
+  const Plan& p = plan_;
+  SpecArgs a;
+  a.N = p.NY;
+  a.lines = p.lines_loc();
+  a.nkz = p.nkz;
+  a.kx0 = p.kx0;
+  a.nkx = p.nkx;
+  a.Kx = p.Kx;
+  a.ax = p.ax;
+  a.az = p.az;
+  a.nu = 1.0 / cfg_.Re;
+  a.mode = mode;
+  if (mode == 1) {
+    a.rk_a = RK3Coef::alpha[n];
+    a.rk_b = RK3Coef::beta[n];
+    a.rk_g = RK3Coef::gamma[n];
+    a.rk_z = RK3Coef::zeta[n];
+  }
+  a.dt = d_dt_;
+  a.Q = cfg_.Q;
+  a.forcing = cfg_.forcing == "parity" ? 1 : 0;
+  a.phi = field_ptr(PHI);
+  a.omega = field_ptr(OMEGA);
+  a.Rphi = field_ptr(RPHI);
+  a.Romega = field_ptr(ROMEGA);
+  for (int i = 0; i < 6; ++i) a.out[i] = field_ptr(OUT0 + i);
+  a.stats = stats ? d_stats_ : nullptr;
+  a.mean_diag = p.owns_mean() ? d_mean_ : nullptr;
+  a.health = cfg_.health_check ? d_health_ : nullptr;
+  if (stats) HIP_CHECK(hipMemsetAsync(d_stats_, 0, 4 * p.NY * sizeof(double), s_comp_));
+  ev(0, false);
+  kspec_launch(ytab_, a, fp64_, s_comp_);
+  ev(0, true);
+  if (stats && comm_) {
+    HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_stats_, 0));
+    comm_->allreduce_sum_f64(d_stats_, 4 * p.NY, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_stats_, s_comm_));
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_stats_, 0));
+  }
+}
+
+void Solver::a2a_backward(int f) {
+  const Plan& p = plan_;
+  const int P = p.P, lines = p.lines_loc();
+  std::vector<size_t> sc(P), so(P), rc(P), ro(P);
+  for (int q = 0; q < P; ++q) {
+    so[q] = static_cast<size_t>(p.y_split.start[q]) * lines * esz_;
+    sc[q] = static_cast<size_t>(p.y_split.count[q]) * lines * esz_;
+    ro[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.start[q] * p.nkz * esz_;
+    rc[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.count[q] * p.nkz * esz_;
+  }
+  const char* send = static_cast<const char*>(field_ptr(OUT0 + f));
+  char* recv = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+  comm_->alltoallv(send, sc, so, recv, rc, ro, s_comm_);
+}
+
+void Solver::a2a_forward(int f) {
+  const Plan& p = plan_;
+  const int P = p.P, lines = p.lines_loc();
+  std::vector<size_t> sc(P), so(P), rc(P), ro(P);
+  for (int q = 0; q < P; ++q) {
+    so[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.start[q] * p.nkz * esz_;
+    sc[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.count[q] * p.nkz * esz_;
+    ro[q] = static_cast<size_t>(p.y_split.start[q]) * lines * esz_;
+    rc[q] = static_cast<size_t>(p.y_split.count[q]) * lines * esz_;
+  }
+  const char* send = static_cast<const char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+  char* recv = static_cast<char*>(field_ptr(OUT0 + f));
+  comm_->alltoallv(send, sc, so, recv, rc, ro, s_comm_);
+}
+
+void Solver::ev(int phase, bool end) {
+  if (!phase_timing_) return;
+  HIP_CHECK(hipEventRecord(ph_ev_[2 * phase + (end ? 1 : 0)], s_comp_));
+  if (end) {
+    HIP_CHECK(hipEventSynchronize(ph_ev_[2 * phase + 1]));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, ph_ev_[2 * phase], ph_ev_[2 * phase + 1]));
+    ph_ms_[phase] += ms;
+  }
+}
+
+std::vector<double> Solver::phase_times_ms() { return ph_ms_; }
+
+void Solver::transforms(int n, bool /*stats*/) {
+  const Plan& p = plan_;
+  XArgs xa;
+  xa.NX = p.NX;
+  xa.nkx = p.nkx;
+  xa.Kx = p.Kx;
+  xa.nkz = p.nkz;
+  xa.ny = p.ny_loc;
+  xa.field_stride_phys = static_cast<long long>(physn_);
+  ZArgs za;
+  za.NX = p.NX;
+  za.Nzp = p.Nzp;
+  za.nkz = p.nkz;
+  za.ny = p.ny_loc;
+  za.y0 = p.y0;
+  za.field_stride = static_cast<long long>(physn_);
+  za.scale = 1.0 / (static_cast<double>(p.NX) * p.Nzp);
+  za.inv_dy = d_invdy_;
+  za.cx = p.ax * p.Kx;
+  za.cz = p.az * p.Kz;
+  za.maxima = d_max_;
+  DtArgs da;
+  da.maxima = d_max_;
+  da.dt = d_dt_;
+  da.time = d_time_;
+  da.dt_log = d_dtlog_;
+  da.cfl = cfg_.cfl;
+  da.dt_max = cfg_.dt_max;
+  da.dt_fixed = cfg_.dt_fixed;
+  da.parity = cfg_.cfl_mode == "parity" ? 1 : 0;
+  da.NX = p.NX;
+  da.NZ = p.NZ;
+  da.LX = cfg_.LX;
+  da.LZ = cfg_.LZ;
+  da.Re = cfg_.Re;
+  da.dy_uniform = 2.0 / (p.NY - 1);
+
+  if (!comm_) {
+    XSrc src;
+    src.base = out_;
+    src.nsrc = 1;
+    src.kx_start[0] = 0;
+    src.kx_start[1] = p.nkx;
+    xa.nfields = 6;
+    xa.field_stride_spec = static_cast<long long>(spec_);
+    ev(1, false);
+    xfft_backward(xa, src, phys_, tw_x_, fp64_, s_comp_);
+    ev(1, true);
+    ev(2, false);
+    zphys(za, phys_, tw_z_, fp64_, s_comp_);
+    ev(2, true);
+    if (n == 0) dt_update(da, s_comp_);
+    XDst dst;
+    dst.base = out_;
+    dst.ndst = 1;
+    dst.kx_start[0] = 0;
+    dst.kx_start[1] = p.nkx;
+    xa.nfields = 3;
+    ev(3, false);
+    xfft_forward(xa, phys_, dst, tw_x_, fp64_, s_comp_);
+    ev(3, true);
+    return;
+  }
+  // ---- P > 1: per-field all-to-all on the comm stream, overlapped with the x transforms ----
+  const int P = p.P;
+  XSrc src;
+  src.base = xbuf_;
+  src.nsrc = P;
+  XDst dst;
+  dst.base = xbuf_;
+  dst.ndst = P;
+  for (int q = 0; q < P; ++q) {
+    src.kx_start[q] = dst.kx_start[q] = p.kx_split.start[q];
+    src.off[q] = dst.off[q] = static_cast<long long>(p.ny_loc) * p.kx_split.start[q] * p.nkz;
+  }
+  src.kx_start[P] = dst.kx_start[P] = p.nkx;
+  xa.nfields = 1;
+  xa.field_stride_spec = static_cast<long long>(xstride_);
+  HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  for (int f = 0; f < 6; ++f) {
+    a2a_backward(f);
+    HIP_CHECK(hipEventRecord(ev_a2a_[f], s_comm_));
+  }
+  for (int f = 0; f < 6; ++f) {
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_a2a_[f], 0));
+    XSrc sf = src;
+    sf.base = static_cast<const char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+    xfft_backward(xa, sf, static_cast<char*>(phys_) + static_cast<size_t>(f) * physn_ * esz_, tw_x_, fp64_, s_comp_);
+  }
+  zphys(za, phys_, tw_z_, fp64_, s_comp_);
+  if (n == 0) {
+    HIP_CHECK(hipEventRecord(ev_phys_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_phys_, 0));
+    comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_red_, s_comm_));
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_red_, 0));
+    dt_update(da, s_comp_);
+  }
+  for (int f = 0; f < 3; ++f) {
+    XDst df = dst;
+    df.base = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+    xfft_forward(xa, static_cast<char*>(phys_) + static_cast<size_t>(f) * physn_ * esz_, df, tw_x_, fp64_, s_comp_);
+    HIP_CHECK(hipEventRecord(ev_xf_[f], s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_xf_[f], 0));
+    a2a_forward(f);
+  }
+  HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+}
+
+void Solver::prepare() {
+  kspec(0, 0, cfg_.stats_every > 0);
+  stats_pending_ = cfg_.stats_every > 0;
+  prepared_ = true;
+}
+
+void Solver::step_body(bool stats) {
+  for (int n = 0; n < 3; ++n) {
+    transforms(n, false);
+    kspec(1, n, stats && n == 2);
+  }
+}
+
+void Solver::step(bool stats_for_next) {
+  if (!prepared_) prepare();
+  const int gi = stats_for_next ? 1 : 0;
+  bool done = false;
+  if (use_graph_ && !debug_sync_enabled() && !phase_timing_) {
+    if (!gexec_[gi] && !graph_ok_[gi]) {
+      try {
+        hipGraph_t g = nullptr;
+        HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeGlobal));
+        try {
+          step_body(stats_for_next);
+        } catch (...) {
+          hipGraph_t junk = nullptr;
+          (void)hipStreamEndCapture(s_comp_, &junk);
+          if (junk) (void)hipGraphDestroy(junk);
+          throw;
+        }
+        HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
+        HIP_CHECK(hipGraphInstantiate(&gexec_[gi], g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+      } catch (const Error& e) {
+        std::cerr << "[channel] hipGraph capture failed, running eagerly: " << e.what() << "\n";
+        (void)hipGetLastError();
+        gexec_[gi] = nullptr;
+        use_graph_ = false;
+      }
+      graph_ok_[gi] = true;
+    }
+    if (gexec_[gi]) {
+      HIP_CHECK(hipGraphLaunch(gexec_[gi], s_comp_));
+      done = true;
+    }
+  }
+  if (!done) step_body(stats_for_next);
+  if (stats_for_next) stats_pending_ = true;
+  ++nstep_;
+}
+
+void Solver::substep_debug(int n) {
+  if (!prepared_) prepare();
+  transforms(n, false);
+  kspec(1, n, false);
+}
+
+void Solver::transforms_debug(bool dt_upd) { transforms(dt_upd ? 0 : 1, false); }
+
+void Solver::synchronize() {
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  HIP_CHECK(hipStreamSynchronize(s_comm_));
+}
+
+void Solver::barrier() {
+  if (comm_) {
+    // tiny allreduce as a device barrier, then host sync
+    comm_->allreduce_max_u32(d_health_, 1, s_comm_);
+    HIP_CHECK(hipStreamSynchronize(s_comm_));
+  }
+  synchronize();
+}
+
+StepLog Solver::log() {
+  synchronize();
+  StepLog L;
+  double dl[8];
+  HIP_CHECK(hipMemcpy(dl, d_dtlog_, sizeof(dl), hipMemcpyDeviceToHost));
+  L.step = nstep_;
+  L.umax = dl[0];
+  L.vmax = dl[1];
+  L.wmax = dl[2];
+  L.cflsum = dl[3];
+  L.dt_c = dl[4];
+  L.dt_v = dl[5];
+  L.dt = dl[6];
+  L.time = dl[7];
+  const int N = plan_.NY;
+  if (plan_.owns_mean()) {
+    double md[4];
+    HIP_CHECK(hipMemcpy(md, d_mean_ + 3 * N, sizeof(md), hipMemcpyDeviceToHost));
+    L.dUdy_lo = md[0];
+    L.dUdy_hi = md[1];
+    L.flux = md[2];
+    L.dpdx = md[3];
+    const double nu = 1.0 / cfg_.Re;
+    L.utau_lo = std::sqrt(nu * std::fabs(L.dUdy_lo));
+    L.utau_hi = std::sqrt(nu * std::fabs(L.dUdy_hi));
+    L.utau = std::sqrt(0.5 * (L.utau_lo * L.utau_lo + L.utau_hi * L.utau_hi));
+  }
+  L.health = health();
+  return L;
+}
+
+unsigned Solver::health() {
+  if (comm_) {
+    comm_->allreduce_max_u32(d_health_, 1, s_comm_);
+    HIP_CHECK(hipStreamSynchronize(s_comm_));
+  }
+  unsigned h = 0;
+  HIP_CHECK(hipMemcpy(&h, d_health_, sizeof(h), hipMemcpyDeviceToHost));
+  return h;
+}
+
+std::vector<double> Solver::stats() {
+  synchronize();
+  std::vector<double> s(4 * plan_.NY);
+  HIP_CHECK(hipMemcpy(s.data(), d_stats_, s.size() * sizeof(double), hipMemcpyDeviceToHost));
+  return s;
+}
+
+std::vector<double> Solver::mean_profile() {
+  synchronize();
+  std::vector<double> U(plan_.NY, 0.0);
+  if (plan_.owns_mean()) HIP_CHECK(hipMemcpy(U.data(), d_mean_, U.size() * sizeof(double), hipMemcpyDeviceToHost));
+  return U;
+}
+
+void Solver::symmetrize() {
+  CH_CHECK(!comm_, "symmetrize: only for P == 1 (P > 1 relies on the per-substep C2R projection)");
+  const Plan& p = plan_;
+  symmetrize_kz0(field_ptr(PHI), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+  symmetrize_kz0(field_ptr(OMEGA), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+  prepared_ = false;
+}
+
+// ---- reference-style run loop with stdout blocks and .dat files --------------------------------
+void Solver::write_logs(const StepLog& L, bool verbose) {
+  if (plan_.rank != 0) return;
+  const int N = plan_.NY, NX = plan_.NX, NZ = plan_.NZ, Nzp = plan_.Nzp;
+  const double nu = 1.0 / cfg_.Re, LY = 2.0, Um = cfg_.Q / LY;
+  const double N2 = static_cast<double>(NX) * Nzp;
+  std::vector<double> U = mean_profile();
+  std::vector<double> Nm(N, 0.0);
+  HIP_CHECK(hipMemcpy(Nm.data(), d_mean_ + N, N * sizeof(double), hipMemcpyDeviceToHost));
+  const double Uc = U[N / 2], ut = L.utau;
+  const auto& y = grid_.y;
+  const double dyc = y[N / 2 + 1] - y[N / 2], dyw = y[1] - y[0];
+  if (verbose) {
+    std::printf("*****RK_STATISTICS****\nmax_V=(%e,%e,%e)\n(dt_c,dt_v)=(%f,%f)\n", L.umax, L.vmax, L.wmax, L.dt_c,
+                L.dt_v);
+    std::printf("(time,counter)=(%f,%ld)\n", L.time, L.step);
+    std::printf("(tau_1,tau_2)=(%e,%e)\n****MEAN_PROFILE_STATISTICS****\n", L.utau_lo, L.utau_hi);
+    std::printf("(RE_t,RE_c,RE_m)=(%e,%e,%e)\n", ut * LY * 0.5 / nu, Uc * 0.5 * LY / nu, 1.0 / nu);
+    std::printf("(Dx+,Dz+)=(%e,%e)\n", 1.5 * ut * cfg_.LX / (nu * NX), 1.5 * ut * cfg_.LZ / (nu * Nzp));
+    std::printf("Dy+(max,min)=(%f,%f)\n", ut * dyc / nu, ut * dyw / nu);
+    std::printf("C_f=%e\n", ut > 0 ? 2.0 * ut * ut / (Um * Um) : 0.0);
+    std::printf("(Um+,Ux+,Um/Uc)=(%f,%f,%f)\n", ut > 0 ? Um / ut : 0.0, ut > 0 ? Uc / ut : 0.0, Uc != 0 ? Um / Uc : 0.0);
+    std::fflush(stdout);
+  }
+  const std::string& pth = cfg_.path;
+  auto app = [&](const char* name) { return std::ofstream(pth + name, std::ios::app); };
+  {
+    auto f = app("MEANPROFILE.dat");
+    for (int j = 0; j < N; ++j) f << " " << std::fixed << U[j] * N2;
+    f << " \n";
+  }
+  {
+    auto f = app("MEANREAYNOLDS.dat");
+    for (int j = 0; j < N; ++j) f << " " << std::fixed << Nm[j] * N2;
+    f << " \n";
+  }
+  {
+    auto f = app("UTAU.dat");
+    f << " " << std::fixed << ut << "\n";
+  }
+  {
+    auto f = app("STATISTICS.dat");
+    f << std::scientific << ut * LY * 0.5 / nu << " " << Uc * 0.5 * LY / nu << " " << 1.0 / nu << " "
+      << (ut > 0 ? Um / ut : 0.0) << " " << (ut > 0 ? Uc / ut : 0.0) << " " << (Uc != 0 ? Um / Uc : 0.0) << " "
+      << 2.0 * ut * ut / (Um * Um) << " " << (Uc != 0 ? 2.0 * ut * ut / (Uc * Uc) : 0.0) << " \n";
+  }
+  {
+    auto f = app("RESOLUTION.dat");
+    f << std::fixed << 1.5 * ut * cfg_.LX / (nu * NX) << " " << 1.5 * ut * cfg_.LZ / (nu * Nzp) << " "
+      << ut * dyc / nu << " " << ut * dyw / nu << "\n";
+  }
+  (void)NZ;
+}
+
+void Solver::write_stats_files(const std::vector<double>& st) {
+  if (plan_.rank != 0) return;
+  const int N = plan_.NY;
+  auto app = [&](const char* name) { return std::ofstream(cfg_.path + name, std::ios::app); };
+  auto sgn_sqrt = [](double x) { return x >= 0 ? std::sqrt(x) : -std::sqrt(-x); };
+  {
+    auto f = app("RSTRSS.dat");
+    for (int j = 0; j < N; ++j) f << " " << std::fixed << sgn_sqrt(-st[3 * N + j]);
+    f << " \n";
+  }
+  const char* names[3] = {"URMS.dat", "VRMS.dat", "WRMS.dat"};
+  for (int s = 0; s < 3; ++s) {
+    auto f = app(names[s]);
+    for (int j = 0; j < N; ++j) f << " " << std::fixed << std::sqrt(std::max(0.0, st[s * N + j]));
+    f << " \n";
+  }
+}
+
+void Solver::run(long nsteps, bool verbose) {
+  if (!prepared_) prepare();
+  const int se = cfg_.stats_every, le = cfg_.log_every, ce = cfg_.checkpoint_every, ye = cfg_.symmetry_every;
+  if (stats_pending_ && se > 0 && nstep_ % se == 0) write_stats_files(stats());
+  stats_pending_ = false;
+  for (long s = 0; s < nsteps; ++s) {
+    const bool want_stats = se > 0 && (nstep_ + 1) % se == 0;
+    step(want_stats);
+    if (want_stats) {
+      write_stats_files(stats());
+      stats_pending_ = false;
+    }
+    const bool do_log = le > 0 && nstep_ % le == 0;
+    if (do_log || (cfg_.health_check && nstep_ % 100 == 0)) {
+      StepLog L = log();
+      if (L.health) {
+        std::fprintf(stderr, "[channel] non-finite state detected at step %ld (t=%g, dt=%g); aborting\n", L.step,
+                     L.time, L.dt);
+        if (comm_) comm_->abort();
+        CH_CHECK(false, "health check failed at step " << L.step);
+      }
+      if (do_log) write_logs(L, verbose);
+    }
+    if (ye > 0 && nstep_ % ye == 0 && !comm_) {
+      symmetrize();
+      prepare();
+    }
+    if (ce > 0 && nstep_ % ce == 0 && cfg_.out_G != "-") {
+      const std::string sfx = "." + std::to_string(nstep_);
+      write_restart(cfg_.out_G + sfx, cfg_.out_DDV + sfx, cfg_.out_UMEAN != "-" ? cfg_.out_UMEAN + sfx : "-");
+    }
+    if (cfg_.t_end > 0 && time() >= cfg_.t_end) break;
+  }
+  synchronize();
+}
+
+// ---- restart I/O (Appendix B) --------------------------------------------------------------------
+void Solver::write_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
+  const Plan& p = plan_;
+  const int N = p.NY, NZ = p.NZ, lines = p.lines_loc();
+  const double N2 = static_cast<double>(p.NX) * p.Nzp;
+  std::vector<std::complex<double>> phi(spec_), om(spec_);
+  std::vector<double> U(N);
+  get_state(phi.data(), om.data(), U.data());
+  double hv[2];
+  HIP_CHECK(hipMemcpy(hv, d_dt_, sizeof(hv), hipMemcpyDeviceToHost));
+  std::vector<int> planes(p.nkx_loc);
+  for (int i = 0; i < p.nkx_loc; ++i) planes[i] = p.kx_fft_pos(p.kx0 + i);
+  auto pack = [&](const std::vector<std::complex<double>>& f) {
+    std::vector<double> d(static_cast<size_t>(p.nkx_loc) * NZ * N * 2, 0.0);
+    for (int i = 0; i < p.nkx_loc; ++i)
+      for (int kz = 0; kz < p.nkz; ++kz)
+        for (int j = 0; j < N; ++j) {
+          const auto v = f[static_cast<size_t>(j) * lines + i * p.nkz + kz] * N2;
+          const size_t o = ((static_cast<size_t>(i) * NZ + kz) * N + j) * 2;
+          d[o] = v.real();
+          d[o + 1] = v.imag();
+        }
+    return d;
+  };
+  std::map<std::string, double> attrs = {{"time", hv[1]}, {"dt", hv[0]}, {"step", static_cast<double>(nstep_)},
+                                         {"Re", cfg_.Re},  {"Q", cfg_.Q},   {"LX", cfg_.LX},
+                                         {"LZ", cfg_.LZ},  {"NX", double(p.NX)}, {"NY", double(N)},
+                                         {"NZ", double(NZ)}, {"format_version", 1.0}};
+  for (int which = 0; which < 2; ++which) {
+    const std::string& path = which == 0 ? g : ddv;
+    if (path.empty() || path == "-") continue;
+    auto data = pack(which == 0 ? om : phi);
+    if (p.rank == 0) {
+      h5_create_field(path, p.NX, N, NZ, false);
+      h5_write_attrs(path, attrs);
+    }
+    for (int r = 0; r < p.P; ++r) {
+      barrier();
+      if (r == p.rank) h5_write_planes(path, planes, data);
+    }
+    barrier();
+  }
+  if (p.owns_mean() && !umean.empty() && umean != "-") {
+    std::vector<double> u(N);
+    for (int j = 0; j < N; ++j) u[j] = U[j] * N2;
+    umean_write(umean, u);
+  }
+  barrier();
+}
+
+void Solver::read_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
+  const Plan& p = plan_;
+  const int N = p.NY, NZ = p.NZ, lines = p.lines_loc();
+  const double N2 = static_cast<double>(p.NX) * p.Nzp;
+  std::vector<int> planes(p.nkx_loc);
+  for (int i = 0; i < p.nkx_loc; ++i) planes[i] = p.kx_fft_pos(p.kx0 + i);
+  std::vector<std::complex<double>> phi(spec_, 0.0), om(spec_, 0.0);
+  auto unpack = [&](const std::string& path, std::vector<std::complex<double>>& f) {
+    std::vector<double> d;
+    int dims[3];
+    h5_read_planes(path, planes, d, dims);
+    CH_CHECK(dims[0] == p.NX && dims[1] == N && dims[2] == 2 * NZ,
+             "restart file " << path << " has dims " << dims[0] << "x" << dims[1] << "x" << dims[2]);
+    for (int i = 0; i < p.nkx_loc; ++i)
+      for (int kz = 0; kz < p.nkz; ++kz)
+        for (int j = 0; j < N; ++j) {
+          const size_t o = ((static_cast<size_t>(i) * NZ + kz) * N + j) * 2;
+          f[static_cast<size_t>(j) * lines + i * p.nkz + kz] = std::complex<double>(d[o], d[o + 1]) / N2;
+        }
+  };
+  unpack(g, om);
+  unpack(ddv, phi);
+  std::vector<double> U(N, 0.0);
+  if (!umean.empty() && umean != "-") {
+    U = umean_read(umean, N);
+    for (auto& u : U) u /= N2;
+  } else {
+    const auto& y = grid_.y;
+    for (int j = 0; j < N; ++j) U[j] = 0.75 * cfg_.Q * (1.0 - y[j] * y[j]);
+  }
+  set_state(phi.data(), om.data(), U.data());
+  auto attrs = h5_read_attrs(g);
+  double t = attrs.count("time") ? attrs["time"] : 0.0, dt = attrs.count("dt") ? attrs["dt"] : 0.0;
+  set_time(t, dt);
+  nstep_ = attrs.count("step") ? static_cast<long>(attrs["step"]) : 0;
+}
+
+}  // namespace channel

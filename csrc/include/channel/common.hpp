@@ -1,0 +1,58 @@
+// Common definitions for the channel_gpu_amd native core (gfx950 / MI355X only).
+//
+// Error handling replaces the reference's check.cu (check.cu:3-79), which printed and called
+// exit(1) on the failing rank only (so peers hung in the next collective).  Here every
+// failure throws a channel::Error; the driver catches it and aborts the whole job (RCCL abort +
+// MPI_Abort), and the Python bindings turn it into a RuntimeError.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+
+namespace channel {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+[[noreturn]] inline void fail(const std::string& msg, const char* file, int line) {
+  std::ostringstream os;
+  os << "channel error at " << file << ":" << line << ": " << msg;
+  throw Error(os.str());
+}
+
+// Debug mode: synchronise after every launch so asynchronous faults are attributed to the kernel
+// that caused them (the reference's kernelCheck ran cudaGetLastError without a sync, check.cu:7).
+bool debug_sync_enabled();
+void set_debug_sync(bool on);
+
+}  // namespace channel
+
+#define CH_CHECK(cond, msg)                                          \
+  do {                                                               \
+    if (!(cond)) {                                                   \
+      std::ostringstream _os;                                        \
+      _os << msg;                                                    \
+      ::channel::fail(_os.str(), __FILE__, __LINE__);                \
+    }                                                                \
+  } while (0)
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      ::channel::fail(std::string(#expr) + " -> " + hipGetErrorString(_e), __FILE__, __LINE__); \
+    }                                                                                     \
+  } while (0)
+
+// After a kernel launch: catch launch-configuration errors immediately, and in debug mode also
+// execution faults.
+#define HIP_LAUNCH_CHECK(stream)                                                          \
+  do {                                                                                    \
+    HIP_CHECK(hipGetLastError());                                                         \
+    if (::channel::debug_sync_enabled()) HIP_CHECK(hipStreamSynchronize(stream));         \
+  } while (0)

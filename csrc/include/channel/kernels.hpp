@@ -1,0 +1,134 @@
+// Host-side launchers for the HIP kernels (implemented in csrc/kernels/*.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "channel/grid.hpp"
+#include "channel/yline_device.hpp"
+
+namespace channel {
+
+// R values the y-line kernels are instantiated for (64*R >= NY).
+int yline_supported_R(int NY);
+
+// Device copies of the per-row coefficient tables (lane-major, see yline_device.hpp).
+struct YTablesDev {
+  double* buf = nullptr;     // single allocation
+  size_t bytes = 0;
+  dev::YTab tab{};
+  int R = 1;
+  void upload(const YGrid& g, int R, hipStream_t stream);
+  void release();
+  ~YTablesDev() { release(); }
+};
+
+// Debug/test entry point: apply one y-line operator to `lines` complex lines stored [y][line].
+enum YLineOp : int {
+  YOP_D1 = 0,        // out = D1 in (compact first derivative)
+  YOP_HELM = 1,      // out = (K - k^2 M)^{-1} M in, out(+-1) = 0 (velocity recovery)
+  YOP_IMPL = 2,      // out = ((1+c k^2) M - c K)^{-1} M in, out(+-1)=0 (implicit viscous step)
+  YOP_MAPPLY = 3,    // out = M in (interior rows, 0 on walls)
+  YOP_KAPPLY = 4,    // out = K in (interior rows, 0 on walls)
+};
+void yline_test(const YTablesDev& t, int op, const void* in, void* out, int lines, const double* k2, double c,
+                bool fp64, hipStream_t stream);
+
+// ---- the fused spectral (y-line) substep kernel ---------------------------------------------
+struct SpecArgs {
+  // geometry
+  int N = 0;              // NY
+  int lines = 0;          // local lines = nkx_loc * nkz, line = ikx_local * nkz + kz
+  int nkz = 0, kx0 = 0, nkx = 0, Kx = 0;
+  double ax = 1, az = 2;  // 2 pi / LX, 2 pi / LZ
+  double nu = 1.0 / 3250.0;
+  // RK3 substep (mode 1)
+  int mode = 0;           // 0 = prepare only (fields from state), 1 = advance + prepare
+  double rk_a = 0, rk_b = 0, rk_g = 0, rk_z = 0;
+  const double* dt = nullptr;   // device scalar
+  // mean flow forcing
+  double Q = 1.8;
+  int forcing = 0;        // 0 implicit (exact flux), 1 parity (constant add)
+  // fields (T2* cast to void*)
+  void* phi = nullptr;
+  void* omega = nullptr;  // line (0,0) holds U(y)
+  void* Rphi = nullptr;
+  void* Romega = nullptr;
+  void* out[6] = {};      // u, v, w, omega_x, omega_y, omega_z ; out[0..2] double as H_x,H_y,H_z input
+  // diagnostics
+  double* stats = nullptr;   // [4][N] plane sums (uu, vv, ww, uv) when non-null
+  double* mean_diag = nullptr;  // [3N + 8]: U, Nx, dU/dy(walls), flux, pressure gradient ...
+  unsigned* health = nullptr;   // bit 0: non-finite state
+};
+void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream);
+
+// ---- FFT stages ---------------------------------------------------------------------------
+// Twiddle table for length n (double and float copies): W_n^m = exp(-2 pi i m / n), m < n.
+struct Twiddles {
+  void* buf = nullptr;
+  int n = 0;
+  bool fp64 = false;
+  void build(int n, bool fp64);
+  void release();
+  ~Twiddles() { release(); }
+};
+
+// Source of a spectral field for the backward x-transform: for P ranks the blocks received from
+// each source rank s hold [y_local][nkx_s][nkz] starting at element offset off[s].
+struct XSrc {
+  const void* base = nullptr;
+  int nsrc = 1;
+  int kx_start[9] = {0};   // global retained-kx start of source s (kx_start[nsrc] = nkx)
+  long long off[8] = {0};  // element offset of source block s
+};
+struct XDst {             // destination blocks for the forward x-transform (per destination rank)
+  void* base = nullptr;
+  int ndst = 1;
+  int kx_start[9] = {0};
+  long long off[8] = {0};
+};
+
+struct XArgs {
+  int NX = 0, nkx = 0, Kx = 0, nkz = 0, ny = 0;   // ny = local y planes
+  int nfields = 1;
+  long long field_stride_spec = 0;   // element stride between fields in the spectral buffers
+  long long field_stride_phys = 0;   // element stride between fields in the physical buffers
+};
+// backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
+void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
+// forward: [y][x][kz] -> spectral truncated kx (unnormalised)
+void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s);
+
+struct ZArgs {
+  int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;
+  long long field_stride = 0;        // element stride between the 6 input fields
+  double scale = 1.0;                // forward normalisation 1/(NX*Nzp)
+  const double* inv_dy = nullptr;    // [NY] 1/local spacing for the CFL estimate
+  double cx = 0, cz = 0;             // kx_max, kz_max for the CFL estimate
+  float* maxima = nullptr;           // [4]: |u|max, |v|max, |w|max, cfl sum max (atomicMax)
+};
+// physical-space stage: 6 fields (u,v,w,wx,wy,wz) [y][x][kz] -> z C2R -> H = u x omega -> z R2C
+// -> truncated H_x,H_y,H_z written in place over fields 0..2.
+void zphys(const ZArgs& a, void* fields, const Twiddles& tw, bool fp64, hipStream_t s);
+
+// standalone FFT entry points for tests: batched C2C along the contiguous axis
+void fft_c2c_test(void* data, int n, int batch, int dir, const Twiddles& tw, bool fp64, hipStream_t s);
+
+// ---- small kernels ---------------------------------------------------------------------------
+struct DtArgs {
+  float* maxima = nullptr;   // [4] from zphys; reset to 0 after use
+  double* dt = nullptr;      // output dt (device)
+  double* time = nullptr;    // accumulated time (device)
+  double* dt_log = nullptr;  // [8]: umax vmax wmax cflsum dt_c dt_v dt ...
+  double cfl = 0.5, dt_max = 0.05, dt_fixed = 0.0;
+  int parity = 0;
+  double NX = 0, NZ = 0, LX = 0, LZ = 0, Re = 0, dy_uniform = 0;
+};
+void dt_update(const DtArgs& a, hipStream_t s);
+
+// kz=0 plane Hermitian symmetrisation of a [y][nkx][nkz] field held entirely by one rank
+void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStream_t s);
+
+}  // namespace channel

@@ -1,0 +1,54 @@
+// Decomposition plan: retained-mode sets, slab split tables and local buffer sizes.
+//
+// Reference: 1-D slab, spectral kx-slabs of NX/P planes and physical y-slabs of NY/P planes
+// (channel.h:71-76), valid only for NX==NY, NY%P==0, NX/P%64==0.
+// Here:
+//  * only the 2/3-rule retained modes are stored: |kx| <= Kx = floor(NX/3), 0 <= kz <= Kz =
+//    floor((2NZ-2)/3) (the dealias mask of dealias.cu:37), 44.5 % of the reference's storage;
+//  * retained kx are kept in compact FFT order  i -> kx = (i <= Kx ? i : i - nkx);
+//  * every split is balanced (counts differ by at most one), so any P <= min(nkx, NY) works,
+//    including NY = 385 at P = 8;
+//  * spectral layout per rank: [y][kx_local][kz] (y outermost, kz fastest): the all-to-all block
+//    for peer p is the contiguous row range y in Y_p, so no local transposes are needed
+//    (the reference ran 5 cublasCgeam passes per transpose, channel_cuda_mpi.c:64-128);
+//  * physical/intermediate layout per rank: [y_local][x][kz].
+#pragma once
+
+#include <cstddef>
+#include <vector>
+
+#include "channel/config.hpp"
+
+namespace channel {
+
+struct Split {
+  int n = 0, parts = 1;
+  std::vector<int> start, count;
+  static Split balanced(int n, int parts);
+  int owner(int idx) const;
+  int max_count() const;
+};
+
+struct Plan {
+  int NX = 0, NY = 0, NZ = 0, Nzp = 0;
+  int Kx = 0, nkx = 0, Kz = 0, nkz = 0;
+  int P = 1, rank = 0;
+  Split kx_split, y_split;
+  int nkx_loc = 0, kx0 = 0;   // local retained-kx range [kx0, kx0 + nkx_loc)
+  int ny_loc = 0, y0 = 0;     // local physical y range
+  int R = 1;                  // rows per lane of the 64-lane y-line solver: 64 * R >= NY
+  double ax = 1.0, az = 2.0;  // 2*pi/LX, 2*pi/LZ
+
+  static Plan make(const Config& cfg, int P, int rank);
+
+  int lines_loc() const { return nkx_loc * nkz; }
+  size_t spec_elems() const { return static_cast<size_t>(NY) * lines_loc(); }
+  size_t phys_elems() const { return static_cast<size_t>(ny_loc) * NX * nkz; }
+  // integer wavenumbers
+  int kx_of(int i_global) const { return i_global <= Kx ? i_global : i_global - nkx; }
+  // position of retained kx index in an NX-point FFT array
+  int kx_fft_pos(int i_global) const { return i_global <= Kx ? i_global : NX - (nkx - i_global); }
+  bool owns_mean() const { return kx0 == 0; }
+};
+
+}  // namespace channel

@@ -1,0 +1,151 @@
+// The channel-flow DNS solver: one instance per rank (one process per GPU).
+//
+// Formulation (reference README.md:4-6): Kim-Moin-Moser phi = lap(v) / omega_y,
+// Fourier x,z with 2/3 dealiasing, compact FD in y, SMR low-storage RK3 with implicit viscous
+// terms, constant flow rate, mean profile U(y) evolved on the rank that owns kx=0.
+//
+// Per RK3 substep (all device-resident, captured into one hipGraph per RK3 step):
+//   K-SPEC (y-lines) -> [all-to-all per field, comm stream] -> x C2C inverse (per field)
+//   -> z physical stage (C2R, u x omega, R2C, CFL maxima) -> x C2C forward (per field)
+//   -> [all-to-all per field] -> next K-SPEC.
+// The reference's equivalent is RKstep (RK3.c:111-193) with host-staged transposes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <complex>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "channel/comm.hpp"
+#include "channel/config.hpp"
+#include "channel/grid.hpp"
+#include "channel/kernels.hpp"
+#include "channel/plan.hpp"
+
+namespace channel {
+
+// SMR low-storage RK3 coefficients (RK3_kernels.cu:24-25, 113; RK3.c:14; meanUevol.c:35-38)
+struct RK3Coef {
+  static constexpr double gamma[3] = {8.0 / 15.0, 5.0 / 12.0, 3.0 / 4.0};
+  static constexpr double zeta[3] = {0.0, -17.0 / 60.0, -5.0 / 12.0};
+  static constexpr double alpha[3] = {29.0 / 96.0, -3.0 / 40.0, 1.0 / 6.0};
+  static constexpr double beta[3] = {37.0 / 160.0, 5.0 / 24.0, 1.0 / 6.0};
+};
+
+struct StepLog {
+  long step = 0;
+  double time = 0, dt = 0, dt_c = 0, dt_v = 0;
+  double umax = 0, vmax = 0, wmax = 0, cflsum = 0;
+  double dUdy_lo = 0, dUdy_hi = 0, flux = 0, dpdx = 0;
+  double utau_lo = 0, utau_hi = 0, utau = 0;
+  unsigned health = 0;
+};
+
+class Solver {
+ public:
+  // nccl_uid: empty for P == 1
+  Solver(const Config& cfg, int rank, int nranks, int device, const std::string& nccl_uid = std::string());
+  ~Solver();
+  Solver(const Solver&) = delete;
+  Solver& operator=(const Solver&) = delete;
+
+  const Config& config() const { return cfg_; }
+  const Plan& plan() const { return plan_; }
+  const YGrid& grid() const { return grid_; }
+  hipStream_t stream() const { return s_comp_; }
+  bool fp64() const { return fp64_; }
+
+  // ---- state --------------------------------------------------------------------------
+  // local spectral state, [y][kx_local][kz] true Fourier coefficients; U: NY (used on the owner)
+  void set_state(const std::complex<double>* phi, const std::complex<double>* omega, const double* U);
+  void get_state(std::complex<double>* phi, std::complex<double>* omega, double* U) const;
+  void init_ic();      // config ic: random | laminar | zero (deterministic, independent of P)
+  void prepare();      // fill the transform inputs from the state (K-SPEC mode 0)
+
+  // ---- time stepping ---------------------------------------------------------------------
+  void step(bool stats_for_next = false);  // one RK3 step
+  void run(long nsteps, bool verbose = true);  // reference-style driver loop with logging/stats
+  void synchronize();
+  StepLog log();                     // reads device diagnostics (host sync)
+  std::vector<double> stats();       // [4][NY] plane sums of the last stats step (global)
+  std::vector<double> mean_profile();  // U(y) (owner rank; zeros elsewhere)
+  unsigned health();                  // global OR of health flags
+  double time() const;
+  long steps_done() const { return nstep_; }
+  void set_time(double t, double dt);
+  void set_use_graph(bool on) { use_graph_ = on; }
+  void set_phase_timing(bool on) { phase_timing_ = on; }
+  std::vector<double> phase_times_ms();  // accumulated per-phase times (phase_timing mode)
+  void symmetrize();                  // kz=0 Hermitian symmetry (P == 1 only)
+
+  // ---- restart files (reference-compatible, Appendix B) --------------------------------
+  void write_restart(const std::string& g, const std::string& ddv, const std::string& umean);
+  void read_restart(const std::string& g, const std::string& ddv, const std::string& umean);
+
+  // ---- raw device access (tests / bindings) ----------------------------------------------
+  enum Field { PHI = 0, OMEGA, RPHI, ROMEGA, OUT0, OUT1, OUT2, OUT3, OUT4, OUT5 };
+  void* field_ptr(int f) const;
+  void* phys_ptr() const { return phys_; }
+  const YTablesDev& ytables() const { return ytab_; }
+  void substep_debug(int n);            // one substep, eager (tests)
+  void transforms_debug(bool dt_update);  // backward + phys + forward only (tests)
+  Comm* comm() { return comm_.get(); }
+  void barrier();
+
+ private:
+  void alloc();
+  void free_all();
+  void transforms(int substep, bool stats);
+  void kspec(int mode, int substep, bool stats);
+  void a2a_backward(int f);
+  void a2a_forward(int f);
+  void step_body(bool stats);
+  void ev(int phase, bool end);
+  void write_logs(const StepLog& L, bool verbose);
+  void write_stats_files(const std::vector<double>& st);
+
+  Config cfg_;
+  Plan plan_;
+  YGrid grid_;
+  bool fp64_ = false;
+  int device_ = 0;
+  size_t esz_ = 8;  // bytes per complex element
+  hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
+  std::unique_ptr<Comm> comm_;
+  YTablesDev ytab_;
+  Twiddles tw_x_, tw_z_;
+
+  void* state_ = nullptr;  // phi, omega, Rphi, Romega (4 * spec)
+  void* out_ = nullptr;    // 6 * spec
+  void* phys_ = nullptr;   // 6 * phys
+  void* xbuf_ = nullptr;   // P>1: 6 * ny_loc*nkx*nkz
+  size_t spec_ = 0, physn_ = 0, xstride_ = 0;
+
+  // device scalars / diagnostics (one allocation)
+  void* dscal_ = nullptr;
+  double* d_dt_ = nullptr;
+  double* d_time_ = nullptr;
+  double* d_dtlog_ = nullptr;
+  float* d_max_ = nullptr;
+  double* d_stats_ = nullptr;
+  double* d_mean_ = nullptr;
+  unsigned* d_health_ = nullptr;
+  double* d_invdy_ = nullptr;
+
+  std::vector<hipEvent_t> ev_a2a_, ev_xf_;
+  hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
+  std::vector<hipEvent_t> ph_ev_;
+  std::vector<double> ph_ms_;
+  bool phase_timing_ = false;
+
+  bool use_graph_ = true;
+  bool graph_ok_[2] = {false, false};
+  hipGraphExec_t gexec_[2] = {nullptr, nullptr};
+  bool prepared_ = false;
+  long nstep_ = 0;
+  bool stats_pending_ = false;
+};
+
+}  // namespace channel

@@ -1,0 +1,671 @@
+// Wall-normal (y-line) kernels: coefficient tables, the fused spectral substep kernel (K-SPEC) and
+// a per-operator test entry point.
+//
+// K-SPEC fuses, per (kx,kz) line, everything the reference does in y between two FFT rounds
+// (SURVEY §7.3 K-SPEC-A/B):
+//   calcHvg/calcHvv (nonLinear_kernels.cu:94-190), rk_step_1/2 (RK3_kernels.cu:6-153),
+//   implicitSolver_double x2 (implicitStep_nu_double.cu:227-247), bilaplaSolver_double
+//   (bilplacSolver_double.cu:320-348: implicit phi, Helmholtz v, D1 v, influence matrix),
+//   meanURKstep_1/2 + forcing (meanUevol.c:201-221, 439-567, on the device for line (0,0)),
+//   calcUW (nonLinear_kernels.cu:8-92), the wz/wx D1 calls and calcOmega
+//   (convolution.c:7-20, convolution_kernels.cu:7-66), calcSt plane sums (statistics.cu:7-95).
+// The reference runs these as ~50 launches + 44 cusparse calls + 8 D2D copies per substep with
+// float<->double casts through HBM.  Here one launch reads 7 fields and writes 10, all y-work is
+// fp64 in registers, and the wall-normal operators are applied in "M-form" (the compact D2 mass
+// matrix multiplies the equation), so the explicit viscous term needs no solve at all.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "channel/common.hpp"
+#include "channel/kernels.hpp"
+#include "channel/yline_device.hpp"
+
+namespace channel {
+
+using namespace dev;
+
+template <typename T>
+struct Cplx;
+template <>
+struct Cplx<float> {
+  using type = float2;
+};
+template <>
+struct Cplx<double> {
+  using type = double2;
+};
+
+int yline_supported_R(int NY) {
+  static const int supported[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16};
+  for (int r : supported)
+    if (64 * r >= NY) return r;
+  CH_CHECK(false, "NY=" << NY << " too large for the y-line kernels (max 1024)");
+}
+
+#define CH_DISPATCH_R(R_, ...)                       \
+  switch (R_) {                                      \
+    case 1: { constexpr int R = 1; __VA_ARGS__; } break;    \
+    case 2: { constexpr int R = 2; __VA_ARGS__; } break;    \
+    case 3: { constexpr int R = 3; __VA_ARGS__; } break;    \
+    case 4: { constexpr int R = 4; __VA_ARGS__; } break;    \
+    case 5: { constexpr int R = 5; __VA_ARGS__; } break;    \
+    case 6: { constexpr int R = 6; __VA_ARGS__; } break;    \
+    case 7: { constexpr int R = 7; __VA_ARGS__; } break;    \
+    case 8: { constexpr int R = 8; __VA_ARGS__; } break;    \
+    case 10: { constexpr int R = 10; __VA_ARGS__; } break;  \
+    case 12: { constexpr int R = 12; __VA_ARGS__; } break;  \
+    case 16: { constexpr int R = 16; __VA_ARGS__; } break;  \
+    default: CH_CHECK(false, "unsupported R=" << R_); \
+  }
+
+// ------------------------------------------------------------------------------------------
+template <int R>
+__global__ void __launch_bounds__(64) d1_factor_kernel(YTab t, double* out) {
+  const int lane = __lane_id();
+  PFac<R> F;
+  CoefD1 cd{t, lane};
+  pfactor<R>(F, cd, lane);
+  pfac_store<R>(F, out, lane);
+}
+
+void YTablesDev::upload(const YGrid& g, int R_, hipStream_t stream) {
+  release();
+  R = R_;
+  const int N = g.N;
+  CH_CHECK(64 * R >= N, "R too small for NY");
+  const int rows = 64 * R;
+  // lane-major reorder: index r*64+lane <- row lane*R + r
+  auto lm = [&](const std::vector<double>& v) {
+    std::vector<double> o(rows, 0.0);
+    for (int lane = 0; lane < 64; ++lane)
+      for (int r = 0; r < R; ++r) {
+        const int j = lane * R + r;
+        o[r * 64 + lane] = j < N ? v[j] : 0.0;
+      }
+    return o;
+  };
+  std::vector<double> mask(N, 0.0);
+  for (int j = 1; j < N - 1; ++j) mask[j] = 1.0;
+  std::vector<std::vector<double>> tabs = {lm(g.d1_lo), lm(g.d1_up), lm(g.d1_rm), lm(g.d1_rc), lm(g.d1_rp),
+                                           lm(g.m_lo),  lm(g.m_up),  lm(g.k_lo),  lm(g.k_c),   lm(g.k_up),
+                                           lm(mask),    lm(g.trap)};
+  int nf = 0;
+  CH_DISPATCH_R(R, nf = PFac<R>::kNumFields);
+  const size_t n = tabs.size() * rows + static_cast<size_t>(nf) * 64;
+  bytes = n * sizeof(double);
+  HIP_CHECK(hipMalloc(&buf, bytes));
+  std::vector<double> host(n, 0.0);
+  for (size_t i = 0; i < tabs.size(); ++i) std::copy(tabs[i].begin(), tabs[i].end(), host.begin() + i * rows);
+  HIP_CHECK(hipMemcpyAsync(buf, host.data(), bytes, hipMemcpyHostToDevice, stream));
+  const double* p = buf;
+  tab.d1_lo = p + 0 * rows;
+  tab.d1_up = p + 1 * rows;
+  tab.d1_rm = p + 2 * rows;
+  tab.d1_rc = p + 3 * rows;
+  tab.d1_rp = p + 4 * rows;
+  tab.m_lo = p + 5 * rows;
+  tab.m_up = p + 6 * rows;
+  tab.k_lo = p + 7 * rows;
+  tab.k_c = p + 8 * rows;
+  tab.k_up = p + 9 * rows;
+  tab.mask = p + 10 * rows;
+  tab.trap = p + 11 * rows;
+  double* fac = buf + tabs.size() * rows;
+  tab.d1fac = fac;
+  for (int i = 0; i < 3; ++i) {
+    tab.w0[i] = g.d1_w0[i];
+    tab.wN[i] = g.d1_wN[i];
+  }
+  tab.N = N;
+  CH_DISPATCH_R(R, hipLaunchKernelGGL(d1_factor_kernel<R>, dim3(1), dim3(64), 0, stream, tab, fac));
+  HIP_LAUNCH_CHECK(stream);
+  HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+void YTablesDev::release() {
+  if (buf) (void)hipFree(buf);
+  buf = nullptr;
+  bytes = 0;
+}
+
+// ---- shared helpers for line kernels --------------------------------------------------------
+template <int R, int K>
+__device__ void d1_apply(const YTab& t, double (&x)[K][R], int lane) {
+  double rhs[K][R];
+  d1_rhs<R, K>(t, x, rhs, lane);
+  PFac<R> F;
+  pfac_load<R>(F, t.d1fac, lane);
+  CoefD1 cd{t, lane};
+  psolve<R, K>(F, cd, rhs, lane);
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[k][r] = rhs[k][r];
+}
+
+template <int R, int K>
+__device__ __forceinline__ void apply_M(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
+  apply_tri<R, K>(t.m_lo, t.mask, t.m_up, x, o, lane);
+}
+template <int R, int K>
+__device__ __forceinline__ void apply_K(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
+  apply_tri<R, K>(t.k_lo, t.k_c, t.k_up, x, o, lane);
+}
+
+// value of complex line at row j (wave-uniform), returned in re/im
+template <int R>
+__device__ __forceinline__ void row_cplx(const double (&x)[2][R], int j, int lane, double& re, double& im) {
+  re = row_value<R>(x[0], j, lane);
+  im = row_value<R>(x[1], j, lane);
+}
+
+// ------------------------------------------------------------------------------------------
+// test kernel: one wave per line, data [y][line] complex, direct global access
+template <int R, typename T>
+__global__ void __launch_bounds__(256) yline_test_kernel(YTab t, int op, const void* vin, void* vout, int lines,
+                                                         const double* k2s, double c) {
+  using T2 = typename Cplx<T>::type;
+  const T2* in = static_cast<const T2*>(vin);
+  T2* out = static_cast<T2*>(vout);
+  const int lane = __lane_id();
+  const int line = blockIdx.x * 4 + threadIdx.x / 64;
+  if (line >= lines) return;  // whole wave exits together
+  const int N = t.N;
+  double x[2][R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = lane * R + r;
+    T2 v = j < N ? in[static_cast<size_t>(j) * lines + line] : T2{0, 0};
+    x[0][r] = j < N ? static_cast<double>(v.x) : 0.0;
+    x[1][r] = j < N ? static_cast<double>(v.y) : 0.0;
+  }
+  const double k2 = k2s ? k2s[line] : 0.0;
+  if (op == YOP_D1) {
+    d1_apply<R, 2>(t, x, lane);
+  } else if (op == YOP_HELM) {
+    double m[2][R];
+    apply_M<R, 2>(t, x, m, lane);
+    PFac<R> F;
+    CoefHelm ch{t, lane, k2};
+    pfactor<R>(F, ch, lane);
+    psolve<R, 2>(F, ch, m, lane);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
+  } else if (op == YOP_IMPL) {
+    double m[2][R];
+    apply_M<R, 2>(t, x, m, lane);
+    PFac<R> F;
+    CoefImpl ci{t, lane, 1.0 + c * k2, c};
+    pfactor<R>(F, ci, lane);
+    psolve<R, 2>(F, ci, m, lane);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
+  } else if (op == YOP_MAPPLY) {
+    double m[2][R];
+    apply_M<R, 2>(t, x, m, lane);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
+  } else if (op == YOP_KAPPLY) {
+    double m[2][R];
+    apply_K<R, 2>(t, x, m, lane);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = lane * R + r;
+    if (j < N) out[static_cast<size_t>(j) * lines + line] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
+  }
+}
+
+void yline_test(const YTablesDev& t, int op, const void* in, void* out, int lines, const double* k2, double c,
+                bool fp64, hipStream_t stream) {
+  dim3 grid((lines + 3) / 4), block(256);
+  if (fp64) {
+    CH_DISPATCH_R(t.R, hipLaunchKernelGGL((yline_test_kernel<R, double>), grid, block, 0, stream, t.tab, op, in, out,
+                                          lines, k2, c));
+  } else {
+    CH_DISPATCH_R(t.R, hipLaunchKernelGGL((yline_test_kernel<R, float>), grid, block, 0, stream, t.tab, op, in, out,
+                                          lines, k2, c));
+  }
+  HIP_LAUNCH_CHECK(stream);
+}
+
+// ------------------------------------------------------------------------------------------
+// K-SPEC: W lines per workgroup (one wave per line); fields staged through an LDS tile
+// [r][lane][line] (pitch W+1 => conflict-free column reads), global access = W consecutive
+// complex values per y row.
+template <int R, typename T, int W>
+struct SpecTile {
+  using T2 = typename Cplx<T>::type;
+  static constexpr int PITCH = W + 1;
+  T2* tile;
+  int N, lines, line0, w, lane;
+
+  __device__ void load(const T2* __restrict__ src, double (&x)[2][R]) const {
+    __syncthreads();
+    for (int e = threadIdx.x; e < N * W; e += W * 64) {
+      const int y = e / W, l = e - y * W;
+      T2 v{0, 0};
+      if (line0 + l < lines) v = src[static_cast<size_t>(y) * lines + line0 + l];
+      const int ly = y / R, r = y - ly * R;
+      tile[(r * 64 + ly) * PITCH + l] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = lane * R + r;
+      const T2 v = tile[(r * 64 + lane) * PITCH + w];
+      x[0][r] = j < N ? static_cast<double>(v.x) : 0.0;
+      x[1][r] = j < N ? static_cast<double>(v.y) : 0.0;
+    }
+  }
+  __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) const {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) tile[(r * 64 + lane) * PITCH + w] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
+    __syncthreads();
+    for (int e = threadIdx.x; e < N * W; e += W * 64) {
+      const int y = e / W, l = e - y * W;
+      if (line0 + l < lines) {
+        const int ly = y / R, r = y - ly * R;
+        dst[static_cast<size_t>(y) * lines + line0 + l] = tile[(r * 64 + ly) * PITCH + l];
+      }
+    }
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void czero(double (&x)[2][R]) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[k][r] = 0.0;
+}
+
+template <int R, typename T, int W>
+__global__ void __launch_bounds__(W * 64) kspec_kernel(YTab t, SpecArgs a) {
+  using T2 = typename Cplx<T>::type;
+  __shared__ T2 tile_mem[64 * R * (W + 1)];
+  double* sred = reinterpret_cast<double*>(tile_mem);  // stats reduction reuses the staging tile
+  static_assert(sizeof(T2) * (W + 1) >= 4 * sizeof(double), "tile too small for the stats reduction");
+  const int lane = __lane_id();
+  const int w = threadIdx.x / 64;
+  const int line0 = blockIdx.x * W;
+  const int line = line0 + w;
+  const bool valid = line < a.lines;
+  const int N = a.N;
+  SpecTile<R, T, W> st{tile_mem, N, a.lines, line0, w, lane};
+
+  const int ikx = valid ? line / a.nkz : 0;
+  const int kz = valid ? line - ikx * a.nkz : 0;
+  const int ig = a.kx0 + ikx;
+  const int kx = ig <= a.Kx ? ig : ig - a.nkx;
+  const double al = a.ax * kx, be = a.az * kz;
+  const double k2 = al * al + be * be;
+  const bool is_mean = valid && kx == 0 && kz == 0;
+  const double inv_k2 = k2 > 0.0 ? 1.0 / k2 : 0.0;
+
+  T2* phi = static_cast<T2*>(a.phi);
+  T2* omega = static_cast<T2*>(a.omega);
+  T2* Rphi = static_cast<T2*>(a.Rphi);
+  T2* Romega = static_cast<T2*>(a.Romega);
+  T2* out[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[i] = static_cast<T2*>(a.out[i]);
+
+  double om[2][R];   // omega (state), U(y) on the mean line
+  double ph[2][R];   // phi (state)
+  double v[2][R];    // wall-normal velocity
+  double dv[2][R];   // dv/dy
+  double mean_diag_flux = 0.0, mean_C = 0.0;
+
+  if (a.mode == 1) {
+    const double dt = *a.dt;
+    double RPn[2][R], RWn[2][R];
+    // ---------------- nonlinear terms h_v, h_g in M-form -----------------------------------
+    {
+      double X[2][R], G[2][R];
+      {
+        double H[2][R];
+        st.load(out[0], H);  // H_x
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          X[0][r] = al * H[1][r];   // -i al Hx
+          X[1][r] = -al * H[0][r];
+          G[0][r] = is_mean ? H[0][r] : -be * H[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
+          G[1][r] = is_mean ? 0.0 : be * H[0][r];
+        }
+        st.load(out[2], H);  // H_z
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          X[0][r] += be * H[1][r];  // -i be Hz
+          X[1][r] -= be * H[0][r];
+          G[0][r] += al * H[1][r];  // -i al Hz
+          G[1][r] -= al * H[0][r];
+        }
+      }
+      d1_apply<R, 2>(t, X, lane);  // D(-i al Hx - i be Hz)
+      {
+        double Hy[2][R];
+        st.load(out[1], Hy);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) X[k][r] -= k2 * Hy[k][r];
+      }
+      apply_M<R, 2>(t, X, RPn, lane);
+      apply_M<R, 2>(t, G, RWn, lane);
+      if (a.mean_diag && is_mean) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = lane * R + r;
+          if (j < N) a.mean_diag[N + j] = G[0][r];
+        }
+      }
+    }
+    // ---------------- explicit part of the RK3 substep in M-form ---------------------------
+    // M rhs = M q + dt [ a_n nu (K q - k^2 M q) + g_n R_now + z_n R_prev ]
+    double rhsP[2][R], rhsW[2][R];
+    {
+      double q[2][R], Mq[2][R], Kq[2][R];
+      st.load(phi, q);
+      apply_M<R, 2>(t, q, Mq, lane);
+      apply_K<R, 2>(t, q, Kq, lane);
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          rhsP[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RPn[k][r]);
+      st.load(omega, q);
+      apply_M<R, 2>(t, q, Mq, lane);
+      apply_K<R, 2>(t, q, Kq, lane);
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          rhsW[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RWn[k][r]);
+      if (a.rk_z != 0.0) {
+        st.load(Rphi, q);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsP[k][r] += dt * a.rk_z * q[k][r];
+        st.load(Romega, q);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsW[k][r] += dt * a.rk_z * q[k][r];
+      }
+    }
+    st.store(Rphi, RPn);
+    st.store(Romega, RWn);
+
+    // ---------------- implicit viscous solves (phi, omega share one factorisation) ---------
+    const double c = a.rk_b * dt * a.nu;
+    double phH[2][R];  // homogeneous phi solutions (real): k=0 -> phi(-1)=1, k=1 -> phi(+1)=1
+    {
+      PFac<R> F;
+      CoefImpl ci{t, lane, 1.0 + c * k2, c};
+      pfactor<R>(F, ci, lane);
+      psolve<R, 2>(F, ci, rhsW, lane);
+      if (is_mean) {
+        // constant flow rate: U += C * U1, U1 = response to a unit mean pressure gradient
+        const double fU = wave_sum<R>([&] {
+          double s = 0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) s += tab(t.trap, r, lane) * rhsW[0][r];
+          return s;
+        }());
+        if (a.forcing == 0) {
+          double U1[1][R], one[1][R], M1[1][R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) one[0][r] = (lane * R + r < N) ? 1.0 : 0.0;
+          apply_tri<R, 1>(t.m_lo, t.mask, t.m_up, one, M1, lane);
+#pragma unroll
+          for (int r = 0; r < R; ++r) U1[0][r] = M1[0][r];
+          psolve<R, 1>(F, ci, U1, lane);
+          const double f1 = wave_sum<R>([&] {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) s += tab(t.trap, r, lane) * U1[0][r];
+            return s;
+          }());
+          mean_C = f1 != 0.0 ? (a.Q - fU) / f1 : 0.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsW[0][r] += mean_C * U1[0][r];
+        } else {
+          // reference forcing (meanUevol.c:201-221): constant added to interior points
+          mean_C = (a.Q - fU) / 2.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsW[0][r] += mean_C * tab(t.mask, r, lane);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) rhsW[1][r] = 0.0;
+        mean_diag_flux = fU;
+      }
+      psolve<R, 2>(F, ci, rhsP, lane);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = lane * R + r;
+        phH[0][r] = (j == 0) ? 1.0 : 0.0;
+        phH[1][r] = (j == N - 1) ? 1.0 : 0.0;
+      }
+      psolve<R, 2>(F, ci, phH, lane);
+    }
+    st.store(omega, rhsW);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) om[k][r] = rhsW[k][r];
+
+    // ---------------- velocity recovery + influence matrix (v(+-1) = v'(+-1) = 0) ----------
+    {
+      PFac<R> F;
+      CoefHelm chm{t, lane, k2};
+      pfactor<R>(F, chm, lane);
+      double vH[2][R];
+      apply_M<R, 2>(t, rhsP, v, lane);
+      psolve<R, 2>(F, chm, v, lane);
+      apply_M<R, 2>(t, phH, vH, lane);
+      psolve<R, 2>(F, chm, vH, lane);
+      double tmp[2][R];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) tmp[k][r] = v[k][r];
+      d1_apply<R, 2>(t, tmp, lane);
+      double p0r, p0i, pNr, pNi;
+      row_cplx<R>(tmp, 0, lane, p0r, p0i);
+      row_cplx<R>(tmp, N - 1, lane, pNr, pNi);
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) tmp[k][r] = vH[k][r];
+      d1_apply<R, 2>(t, tmp, lane);
+      // homogeneous wall derivatives: tmp[0] = dv_h1 (phi(-1)=1), tmp[1] = dv_h2 (phi(+1)=1)
+      const double h10 = row_value<R>(tmp[0], 0, lane), h1N = row_value<R>(tmp[0], N - 1, lane);
+      const double h20 = row_value<R>(tmp[1], 0, lane), h2N = row_value<R>(tmp[1], N - 1, lane);
+      const double det = h10 * h2N - h20 * h1N;
+      const bool apply = !is_mean && k2 > 0.0 && dt > 1e-14 && det != 0.0;
+      const double id = apply ? 1.0 / det : 0.0;
+      // [h10 h20; h1N h2N] [C1; C2] = -[p0; pN]
+      const double C1r = (-p0r * h2N + h20 * pNr) * id, C1i = (-p0i * h2N + h20 * pNi) * id;
+      const double C2r = (-h10 * pNr + h1N * p0r) * id, C2i = (-h10 * pNi + h1N * p0i) * id;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ph[0][r] = rhsP[0][r] + C1r * phH[0][r] + C2r * phH[1][r];
+        ph[1][r] = rhsP[1][r] + C1i * phH[0][r] + C2i * phH[1][r];
+        v[0][r] += C1r * vH[0][r] + C2r * vH[1][r];
+        v[1][r] += C1i * vH[0][r] + C2i * vH[1][r];
+      }
+      if (is_mean || k2 == 0.0) {
+        czero<R>(ph);
+        czero<R>(v);
+      }
+    }
+    st.store(phi, ph);
+  } else {
+    // ---------------- prepare only: fields from the state ----------------------------------
+    st.load(phi, ph);
+    st.load(omega, om);
+    PFac<R> F;
+    CoefHelm chm{t, lane, k2};
+    pfactor<R>(F, chm, lane);
+    apply_M<R, 2>(t, ph, v, lane);
+    psolve<R, 2>(F, chm, v, lane);
+    if (is_mean || k2 == 0.0) {
+      czero<R>(ph);
+      czero<R>(v);
+    }
+  }
+
+  // ---------------- health check (non-finite state) -----------------------------------------
+  if (a.health) {
+    bool bad = false;
+#pragma unroll
+    for (int r = 0; r < R; ++r) bad |= !isfinite(ph[0][r]) || !isfinite(ph[1][r]) || !isfinite(om[0][r]) || !isfinite(om[1][r]);
+    if (__any(bad) && lane == 0) atomicOr(a.health, 1u);
+  }
+
+  // ---------------- prepare velocity / vorticity for the physical-space stage ----------------
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) dv[k][r] = v[k][r];
+  d1_apply<R, 2>(t, dv, lane);
+  double Dom[2][R];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) Dom[k][r] = om[k][r];
+  d1_apply<R, 2>(t, Dom, lane);
+
+  double fu[2][R], fw[2][R];
+  // u = i (al dv - be om)/k2 ; w = i (be dv + al om)/k2   (nonLinear_kernels.cu:55-72)
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const double ar = (al * dv[0][r] - be * om[0][r]) * inv_k2, ai = (al * dv[1][r] - be * om[1][r]) * inv_k2;
+    const double br = (be * dv[0][r] + al * om[0][r]) * inv_k2, bi = (be * dv[1][r] + al * om[1][r]) * inv_k2;
+    fu[0][r] = -ai; fu[1][r] = ar;
+    fw[0][r] = -bi; fw[1][r] = br;
+  }
+  if (is_mean) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      fu[0][r] = om[0][r];  // U(y)
+      fu[1][r] = 0.0;
+      fw[0][r] = 0.0;
+      fw[1][r] = 0.0;
+    }
+  }
+  // plane statistics (statistics.cu:7-95), fluctuations only, weight 2 for kz > 0
+  if (a.stats) {
+    __syncthreads();  // the tile may still be read by the previous staging store
+    for (int i = threadIdx.x; i < 4 * 64 * R; i += W * 64) sred[i] = 0.0;
+    __syncthreads();
+    if (valid && !is_mean) {
+      const double wgt = kz == 0 ? 1.0 : 2.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int idx = r * 64 + lane;
+        atomicAdd(&sred[0 * 64 * R + idx], wgt * (fu[0][r] * fu[0][r] + fu[1][r] * fu[1][r]));
+        atomicAdd(&sred[1 * 64 * R + idx], wgt * (v[0][r] * v[0][r] + v[1][r] * v[1][r]));
+        atomicAdd(&sred[2 * 64 * R + idx], wgt * (fw[0][r] * fw[0][r] + fw[1][r] * fw[1][r]));
+        atomicAdd(&sred[3 * 64 * R + idx], wgt * (fu[0][r] * v[0][r] + fu[1][r] * v[1][r]));
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * 64 * R; i += W * 64) {
+      const int s = i / (64 * R), rem = i - s * 64 * R, r = rem / 64, l = rem - r * 64;
+      const int j = l * R + r;
+      if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
+    }
+  }
+  st.store(out[0], fu);
+  st.store(out[1], v);
+  st.store(out[2], fw);
+  // vorticity: wx = Dw - i be v ; wy = omega ; wz = i al v - Du   (convolution_kernels.cu:46-53)
+  // D(dv) = D2 v = phi + k2 v (Helmholtz identity, consistent with the compact D2 operator)
+  {
+    double wx[2][R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double DDr = ph[0][r] + k2 * v[0][r], DDi = ph[1][r] + k2 * v[1][r];
+      const double br = (be * DDr + al * Dom[0][r]) * inv_k2, bi = (be * DDi + al * Dom[1][r]) * inv_k2;
+      wx[0][r] = -bi + be * v[1][r];
+      wx[1][r] = br - be * v[0][r];
+      if (is_mean) { wx[0][r] = 0.0; wx[1][r] = 0.0; }
+    }
+    st.store(out[3], wx);
+  }
+  {
+    double wy[2][R];  // omega_y; zero on the mean line (whose omega slot holds U)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) wy[k][r] = is_mean ? 0.0 : om[k][r];
+    st.store(out[4], wy);  // every wave reaches every staging barrier
+  }
+  {
+    double wz[2][R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double DDr = ph[0][r] + k2 * v[0][r], DDi = ph[1][r] + k2 * v[1][r];
+      const double ar = (al * DDr - be * Dom[0][r]) * inv_k2, ai = (al * DDi - be * Dom[1][r]) * inv_k2;
+      // Du = i(ar + i ai) = -ai + i ar ; wz = i al v - Du
+      wz[0][r] = -al * v[1][r] + ai;
+      wz[1][r] = al * v[0][r] - ar;
+      if (is_mean) { wz[0][r] = -Dom[0][r]; wz[1][r] = 0.0; }
+    }
+    st.store(out[5], wz);
+  }
+  if (a.mean_diag && is_mean) {
+    const double d0 = row_value<R>(Dom[0], 0, lane), dN = row_value<R>(Dom[0], N - 1, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int j = lane * R + r;
+      if (j < N) a.mean_diag[j] = om[0][r];
+    }
+    if (lane == 0) {
+      a.mean_diag[3 * N + 0] = d0;
+      a.mean_diag[3 * N + 1] = dN;
+      a.mean_diag[3 * N + 2] = mean_diag_flux;
+      a.mean_diag[3 * N + 3] = mean_C;
+    }
+  }
+}
+
+template <int R, typename T>
+constexpr int kspec_waves() {
+  return (R <= 4 && 64 * R * 9 * 2 * sizeof(T) <= 64 * 1024) ? 8 : 4;
+}
+
+template <int R, typename T>
+static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
+  constexpr int W = kspec_waves<R, T>();
+  dim3 grid((a.lines + W - 1) / W), block(W * 64);
+  hipLaunchKernelGGL((kspec_kernel<R, T, W>), grid, block, 0, stream, t.tab, a);
+}
+
+void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream) {
+  CH_CHECK(a.N == t.tab.N, "kspec: NY mismatch with tables");
+  if (fp64) {
+    CH_DISPATCH_R(t.R, kspec_launch_t<R, double>(t, a, stream));
+  } else {
+    CH_DISPATCH_R(t.R, kspec_launch_t<R, float>(t, a, stream));
+  }
+  HIP_LAUNCH_CHECK(stream);
+}
+
+}  // namespace channel

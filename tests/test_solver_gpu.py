@@ -1,0 +1,122 @@
+"""End-to-end GPU solver tests against the NumPy fp64 oracle and analytic solutions."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from channel_gpu_amd.reference import oracle as ora
+from channel_gpu_amd.utils.config import default_config
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300)
+
+
+def make_solver(native, **kw):
+    cfg = default_config(**kw)
+    return native.Solver(cfg, 0, 1, 0, b"")
+
+
+@pytest.mark.parametrize("NX,NY,NZ", [(32, 33, 17), (32, 65, 33)])
+def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision="fp64", dt_fixed=0.01, stats_every=0, log_every=0,
+              symmetry_every=0, ic="zero")
+    s = make_solver(native, **kw)
+    o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=0.01)
+    phi, om = ora.random_state(o.plan, o.ops, seed=3, amp=0.3)
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    o.set_state(phi, om, U)
+    s.set_state(phi, om, U)
+    s.prepare()
+    for it in range(3):
+        o.step()
+        s.step(False)
+        gphi, gom, gU = s.get_state()
+        assert rel(gphi, o.phi) < 1e-9, f"phi step {it}"
+        assert rel(gom, o.om) < 1e-9, f"omega step {it}"
+        assert rel(gU, o.U) < 1e-11, f"U step {it}"
+
+
+def test_poiseuille_steady(native):
+    """BASELINE config 1 on the GPU path: the laminar profile 1.35(1-y^2) is a steady state."""
+    s = make_solver(native, NX=32, NY=33, NZ=17, Re=100.0, precision="fp64", ic="laminar", stats_every=0,
+                    log_every=0, symmetry_every=0)
+    s.init_ic()
+    s.prepare()
+    for _ in range(20):
+        s.step(False)
+    y = np.asarray(s.grid.y)
+    U = np.asarray(s.mean_profile())
+    assert np.max(np.abs(U - 1.35 * (1 - y * y))) < 1e-10
+    L = s.log()
+    assert abs(L.utau ** 2 - 2.7 / 100.0) < 1e-8
+    assert L.health == 0
+
+
+def test_poiseuille_relaxation(native):
+    """From a blunt profile with the same flux, the mean flow relaxes to the parabola."""
+    s = make_solver(native, NX=32, NY=33, NZ=17, Re=100.0, precision="fp64", ic="zero", stats_every=0,
+                    log_every=0, symmetry_every=0, dt_fixed=2.0)
+    y = np.asarray(s.grid.y)
+    U0 = 1.0 - y ** 8
+    U0 *= 1.8 / np.trapz(U0, y)
+    n = s.plan.NY * s.plan.nkx_loc * s.plan.nkz
+    z = np.zeros(n, complex)
+    s.set_state(z, z, U0)
+    s.prepare()
+    for _ in range(300):
+        s.step(False)
+    U = np.asarray(s.mean_profile())
+    assert np.max(np.abs(U - 1.35 * (1 - y * y))) < 1e-6
+
+
+def test_graph_equals_eager_fp32(native):
+    kw = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp32", ic="random", ic_amplitude=0.2, stats_every=0,
+              log_every=0, symmetry_every=0)
+    a = make_solver(native, **kw)
+    b = make_solver(native, **kw)
+    b.set_use_graph(False)
+    for s in (a, b):
+        s.init_ic()
+        s.prepare()
+        for _ in range(4):
+            s.step(False)
+    pa, oa, ua = a.get_state()
+    pb, ob, ub = b.get_state()
+    assert np.array_equal(pa, pb) and np.array_equal(oa, ob) and np.array_equal(ua, ub)
+    assert np.isfinite(pa).all() and a.health() == 0
+
+
+def test_turbulent_smoke_128(native, tmp_path):
+    """Reference grid 128x129x128 (Re_tau~180 box) in fp32: finite, flux held, stats files written."""
+    s = make_solver(native, NX=128, NY=129, NZ=65, Re=3250.0, precision="fp32", ic="random", ic_amplitude=0.3,
+                    stats_every=2, log_every=2, path=str(tmp_path) + "/")
+    s.init_ic()
+    s.run(6, False)
+    L = s.log()
+    assert L.health == 0 and L.dt > 0 and np.isfinite(L.utau)
+    assert abs(L.flux - 1.8) < 0.05  # flux before the correction of the last substep
+    for f in ["MEANPROFILE.dat", "UTAU.dat", "STATISTICS.dat", "URMS.dat", "RSTRSS.dat"]:
+        assert (tmp_path / f).exists(), f
+
+
+def test_restart_roundtrip(native, tmp_path):
+    if not native.hdf5_available():
+        pytest.skip("libhdf5 unavailable")
+    kw = dict(NX=32, NY=33, NZ=17, Re=400.0, precision="fp32", ic="random", stats_every=0, log_every=0)
+    a = make_solver(native, **kw)
+    a.init_ic()
+    a.prepare()
+    a.step(False)
+    g, d, u = str(tmp_path / "G.h5"), str(tmp_path / "DDV.h5"), str(tmp_path / "U.bin")
+    a.write_restart(g, d, u)
+    b = make_solver(native, **kw)
+    b.read_restart(g, d, u)
+    pa, oa, ua = a.get_state()
+    pb, ob, ub = b.get_state()
+    assert rel(pb, pa) < 1e-6 and rel(ob, oa) < 1e-6 and rel(ub, ua) < 1e-6
+    assert abs(b.time() - a.time()) < 1e-12
