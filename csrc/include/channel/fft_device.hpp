@@ -1,8 +1,13 @@
-// In-LDS batched complex FFT (Stockham autosort, radix-4 passes + one radix-2 pass when log2 N is
-// odd).  All threads of the workgroup cooperate on ROWS rows of length N held in LDS; each pass
-// gathers its butterfly inputs into registers, synchronises, and writes the outputs back to the
-// same LDS rows (in-place through registers), so a tile needs only one LDS buffer.
-// Twiddles come from a global table W_N^m = exp(-2 pi i m / N) (L1/L2 resident).
+// In-LDS batched complex FFT (Stockham autosort, mixed radix 16/8/4/2, radix-16 first).
+//
+// All threads of the workgroup cooperate on ROWS rows of length N held in LDS.  Each pass gathers
+// its butterfly inputs into registers, synchronises, applies the inter-pass twiddles and an R-point
+// DFT in registers, and writes the outputs back in place.  LDS addresses are padded by one slot per
+// 16 elements (fft_pidx): with radix-16 first passes every store lane-stride becomes 17 elements
+// (34 dwords), which is conflict-free for ds_write_b64, and the strided reads stay contiguous.
+// Radix plans: 16, 16x2, 16x4, 16x8, 16x16, 16x16x2, 16x16x4, 16x16x8 (N = 16 ... 2048): at most
+// three LDS round trips per transform (the radix-4-only version needed log4 N + 1).
+// Twiddles W_N^m = exp(-2 pi i m / N) come from a global table (L1/L2 resident).
 //
 // Replaces the reference's cuFFT 2-D plans (fft.c:17-23); length is a compile-time power of two.
 #pragma once
@@ -35,97 +40,180 @@ template <typename T2>
 __device__ __forceinline__ T2 csub(T2 a, T2 b) {
   return T2{a.x - b.x, a.y - b.y};
 }
+// multiply by -i (forward) or +i (inverse)
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 mul_mi(T2 d) {
+  return INV ? T2{-d.y, d.x} : T2{d.y, -d.x};
+}
 
 constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
 
+// padded LDS index of logical element p of a row
+__device__ __forceinline__ constexpr int fft_pidx(int p) { return p + (p >> 4); }
+template <int N>
+struct FftPitch {
+  static constexpr int value = N + N / 16 + (N >= 16 ? 0 : 1);
+};
+
+// ---- register DFTs (in place, natural order) --------------------------------------------------
 template <bool INV, typename T2>
-__device__ __forceinline__ void radix4(T2 (&v)[4]) {
+__device__ __forceinline__ void dft2(T2* v) {
+  const T2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft4(T2* v) {
   const T2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
   const T2 a2 = cadd(v[1], v[3]);
-  const T2 d = csub(v[1], v[3]);
-  // forward: a3 = -i d ; inverse: a3 = +i d
-  const T2 a3 = INV ? T2{-d.y, d.x} : T2{d.y, -d.x};
+  const T2 a3 = mul_mi<INV>(csub(v[1], v[3]));
   v[0] = cadd(a0, a2);
   v[1] = cadd(a1, a3);
   v[2] = csub(a0, a2);
   v[3] = csub(a1, a3);
 }
 
-template <int N, int ROWS, int NT, bool INV, typename T2>
-__device__ void lds_fft(T2* __restrict__ buf, int pitch, const T2* __restrict__ tw, int tid) {
-  constexpr int LOG = ilog2(N);
-  constexpr int Q = N / 4;
-  constexpr int NB4 = ROWS * Q;
-  constexpr int B4 = (NB4 + NT - 1) / NT;
+// DFT of length 4*Q computed as Q-point... (generic two-level decomposition R = 4 x S)
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft8(T2* v) {
+  using T = decltype(v[0].x);
+  const T h = static_cast<T>(0.70710678118654752440);
+  // stage 1: DFT4 over n = 2 n1 + n2 for fixed n2
+  T2 a[2][4];
 #pragma unroll
-  for (int pass = 0; pass < LOG / 2; ++pass) {
-    const int Ns = 1 << (2 * pass);
-    T2 v[B4][4];
+  for (int n2 = 0; n2 < 2; ++n2) {
 #pragma unroll
-    for (int b = 0; b < B4; ++b) {
-      const int idx = tid + b * NT;
-      if (NB4 % NT == 0 || idx < NB4) {
-        const int row = idx / Q, j = idx - row * Q;
-        const T2* p = buf + row * pitch + j;
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[2 * n1 + n2];
+    dft4<INV>(a[n2]);
+  }
+  // twiddles W8^(n2*k1) for n2 = 1
+  // k1=1: W8^1 = (h, -h) fwd ; k1=2: -i ; k1=3: W8^3 = (-h, -h)
+  {
+    T2 x = a[1][1];
+    a[1][1] = INV ? T2{h * (x.x - x.y), h * (x.x + x.y)} : T2{h * (x.x + x.y), h * (x.y - x.x)};
+    a[1][2] = mul_mi<INV>(a[1][2]);
+    x = a[1][3];
+    a[1][3] = INV ? T2{-h * (x.x + x.y), h * (x.x - x.y)} : T2{h * (x.y - x.x), -h * (x.x + x.y)};
+  }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[b][r] = p[r * Q];
-      }
+  for (int k1 = 0; k1 < 4; ++k1) {
+    v[k1] = cadd(a[0][k1], a[1][k1]);
+    v[k1 + 4] = csub(a[0][k1], a[1][k1]);
+  }
+}
+
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft16(T2* v) {
+  using T = decltype(v[0].x);
+  // n = 4 n1 + n2, k = k1 + 4 k2
+  T2 a[4][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+    dft4<INV>(a[n2]);
+  }
+  // twiddles W16^(n2*k1)
+  const T c1 = static_cast<T>(0.92387953251128675613), s1 = static_cast<T>(0.38268343236508977173);
+  const T h = static_cast<T>(0.70710678118654752440);
+  const T sg = INV ? T(1) : T(-1);  // sign of the sine part
+  const T cs[10] = {T(1), c1, h, s1, T(0), -s1, -h, -c1, T(-1), -c1};
+  const T sn[10] = {T(0), s1, h, c1, T(1), c1, h, s1, T(0), -s1};
+#pragma unroll
+  for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1) {
+      const int m = n2 * k1;
+      const T2 w{cs[m], sg * sn[m]};
+      a[n2][k1] = cmul(a[n2][k1], w);
     }
-    __syncthreads();
 #pragma unroll
-    for (int b = 0; b < B4; ++b) {
-      const int idx = tid + b * NT;
-      if (NB4 % NT == 0 || idx < NB4) {
-        const int row = idx / Q, j = idx - row * Q;
-        const int k = j & (Ns - 1);
-        if (pass > 0) {
-          const int stride = N / (4 * Ns);
+  for (int k1 = 0; k1 < 4; ++k1) {
+    T2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+    dft4<INV>(b);
 #pragma unroll
-          for (int r = 1; r < 4; ++r) {
-            T2 w = tw[k * r * stride];
-            if (INV) w.y = -w.y;
-            v[b][r] = cmul(v[b][r], w);
-          }
+    for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+  }
+}
+
+template <int R, bool INV, typename T2>
+__device__ __forceinline__ void dftR(T2* v) {
+  if constexpr (R == 2) dft2<INV>(v);
+  else if constexpr (R == 4) dft4<INV>(v);
+  else if constexpr (R == 8) dft8<INV>(v);
+  else dft16<INV>(v);
+}
+
+// ---- one Stockham pass --------------------------------------------------------------------
+template <int N, int R, int NS, int ROWS, int PITCH, int NT, bool INV, typename T2>
+__device__ __forceinline__ void stockham_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int tid) {
+  constexpr int Q = N / R;
+  constexpr int NB = ROWS * Q;
+  constexpr int B = (NB + NT - 1) / NT;
+  T2 v[B][R];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int idx = tid + b * NT;
+    if (NB % NT == 0 || idx < NB) {
+      const int row = idx / Q, j = idx - row * Q;
+      const T2* p = buf + row * PITCH;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(j + r * Q)];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int idx = tid + b * NT;
+    if (NB % NT == 0 || idx < NB) {
+      const int row = idx / Q, j = idx - row * Q;
+      const int k = j & (NS - 1);
+      if constexpr (NS > 1) {
+        constexpr int stride = N / (R * NS);
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          T2 w = tw[k * r * stride];
+          if (INV) w.y = -w.y;
+          v[b][r] = cmul(v[b][r], w);
         }
-        radix4<INV>(v[b]);
-        T2* p = buf + row * pitch + (j - k) * 4 + k;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) p[r * Ns] = v[b][r];
       }
+      dftR<R, INV>(v[b]);
+      T2* p = buf + row * PITCH;
+      const int base = (j - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) p[fft_pidx(base + r * NS)] = v[b][r];
     }
-    __syncthreads();
   }
-  if constexpr (LOG % 2 == 1) {
-    constexpr int H = N / 2;
-    constexpr int NB2 = ROWS * H;
-    constexpr int B2 = (NB2 + NT - 1) / NT;
-    constexpr int Ns = N / 2;  // final radix-2 pass
-    T2 v[B2][2];
-#pragma unroll
-    for (int b = 0; b < B2; ++b) {
-      const int idx = tid + b * NT;
-      if (NB2 % NT == 0 || idx < NB2) {
-        const int row = idx / H, j = idx - row * H;
-        v[b][0] = buf[row * pitch + j];
-        v[b][1] = buf[row * pitch + j + H];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < B2; ++b) {
-      const int idx = tid + b * NT;
-      if (NB2 % NT == 0 || idx < NB2) {
-        const int row = idx / H, j = idx - row * H;
-        const int k = j & (Ns - 1);  // = j
-        T2 w = tw[k];
-        if (INV) w.y = -w.y;
-        const T2 x1 = cmul(v[b][1], w);
-        buf[row * pitch + k] = cadd(v[b][0], x1);
-        buf[row * pitch + k + Ns] = csub(v[b][0], x1);
-      }
-    }
-    __syncthreads();
-  }
+  __syncthreads();
+}
+
+// radix plan: 16 first, then 16, then the remainder
+template <int N>
+struct FftPlan {
+  static constexpr int L = ilog2(N);
+  static constexpr int R0 = N >= 16 ? 16 : N;
+  static constexpr int R1 = N >= 256 ? 16 : (N / R0 > 1 ? N / R0 : 1);
+  static constexpr int R2 = N / (R0 * R1) > 1 ? N / (R0 * R1) : 1;
+  static_assert(R0 * R1 * R2 == N, "unsupported FFT length");
+  static_assert(R2 <= 16, "FFT length too large");
+};
+
+// Rows are at buf + row*PITCH, element x of a row at fft_pidx(x).  Ends with a barrier.
+template <int N, int ROWS, int PITCH, int NT, bool INV, typename T2>
+__device__ void lds_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int tid) {
+  using Pl = FftPlan<N>;
+  stockham_pass<N, Pl::R0, 1, ROWS, PITCH, NT, INV>(buf, tw, tid);
+  if constexpr (Pl::R1 > 1) stockham_pass<N, Pl::R1, Pl::R0, ROWS, PITCH, NT, INV>(buf, tw, tid);
+  if constexpr (Pl::R2 > 1) stockham_pass<N, Pl::R2, Pl::R0 * Pl::R1, ROWS, PITCH, NT, INV>(buf, tw, tid);
+}
+
+// XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD under the
+// observed round-robin dispatch, so logical tiles that are adjacent in memory are given to blocks
+// on the same XCD (their partial cache lines then merge in one L2).  Bijective for any n.
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned n) {
+  const unsigned q = n / 8, r = n % 8, x = b % 8, i = b / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
 }  // namespace dev

@@ -70,6 +70,8 @@ struct YTab {
   const double* mask;    // 1 on interior rows, 0 on walls and padding
   const double* trap;    // trapezoid weights (0 on padding)
   const double* d1fac;   // D1 factorisation table [nf][64]
+  const double* d1row0;  // first row of the dense D1 = A1^-1 B1 (wall derivative at y=-1)
+  const double* d1rowN;  // last row (wall derivative at y=+1)
   double w0[3], wN[3];   // D1 wall closures
   int N;
 };
@@ -350,6 +352,14 @@ __device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][
     for (int r = 0; r < R; ++r)
       if (lane == lN && r == rN) out[k][r] = t.wN[0] * g0 + t.wN[1] * g1 + t.wN[2] * g2;
   }
+}
+
+template <int K>
+__device__ __forceinline__ void wave_sum_n(double (&v)[K]) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1)
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += bperm(v[k], (__lane_id() ^ s));
 }
 
 template <int R>

@@ -54,7 +54,9 @@ template <int NX, typename T>
 struct XCfg {
   static constexpr int C = sizeof(T) == 4 ? (NX >= 1024 ? 8 : 16) : (NX >= 1024 ? 4 : 8);
   static constexpr int NT = 256;
-  static constexpr int PITCH = NX + (sizeof(T) == 4 ? 2 : 1);
+  // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
+  // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
+  static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
 };
 
 __device__ __forceinline__ int find_block(const int* start, int n, int i) {
@@ -71,30 +73,44 @@ __global__ void __launch_bounds__(256) xfft_backward_kernel(XArgs a, XSrc src, t
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   __shared__ T2 s[C * PITCH];
-  const int y = blockIdx.x, kz0 = blockIdx.y * C, f = blockIdx.z;
+  const int nkzc = (a.nkz + C - 1) / C;
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);  // adjacent kz chunks of one (y, f) share an XCD
+  const int kz0 = static_cast<int>(t % nkzc) * C;
+  const int rest = static_cast<int>(t / nkzc);
+  const int y = rest % a.ny, f = rest / a.ny;
   const int tid = threadIdx.x;
   const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
-  for (int e = tid; e < NX * C; e += NT) {
+  // issue every global load of this thread before touching LDS (one latency, not EPT of them)
+  constexpr int EPT = (NX * C + NT - 1) / NT;
+  T2 v[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NT;
     const int x = e / C, c = e - x * C;
     const int kz = kz0 + c;
     int i = -1;
     if (x <= a.Kx) i = x;
     else if (x >= NX - a.Kx) i = a.nkx - (NX - x);
-    T2 v{0, 0};
-    if (i >= 0 && kz < a.nkz) {
+    v[q] = T2{0, 0};
+    if (e < NX * C && i >= 0 && kz < a.nkz) {
       const int sb = find_block(src.kx_start, src.nsrc, i);
       const int nk = src.kx_start[sb + 1] - src.kx_start[sb];
-      v = base[src.off[sb] + (static_cast<long long>(y) * nk + (i - src.kx_start[sb])) * a.nkz + kz];
+      v[q] = base[src.off[sb] + (static_cast<long long>(y) * nk + (i - src.kx_start[sb])) * a.nkz + kz];
     }
-    s[c * PITCH + x] = v;
+  }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NT;
+    const int x = e / C, c = e - x * C;
+    if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
   }
   __syncthreads();
-  lds_fft<NX, C, NT, true>(s, PITCH, tw, tid);
+  lds_fft<NX, C, PITCH, NT, true>(s, tw, tid);
   T2* out = phys + f * a.field_stride_phys;
   for (int e = tid; e < NX * C; e += NT) {
     const int x = e / C, c = e - x * C;
     const int kz = kz0 + c;
-    if (kz < a.nkz) out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + x];
+    if (kz < a.nkz) out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
   }
 }
 
@@ -105,18 +121,31 @@ __global__ void __launch_bounds__(256) xfft_forward_kernel(XArgs a, const typena
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   __shared__ T2 s[C * PITCH];
-  const int y = blockIdx.x, kz0 = blockIdx.y * C, f = blockIdx.z;
+  const int nkzc = (a.nkz + C - 1) / C;
+  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
+  const int kz0 = static_cast<int>(t % nkzc) * C;
+  const int rest = static_cast<int>(t / nkzc);
+  const int y = rest % a.ny, f = rest / a.ny;
   const int tid = threadIdx.x;
   const T2* in = phys + f * a.field_stride_phys;
-  for (int e = tid; e < NX * C; e += NT) {
+  constexpr int EPT = (NX * C + NT - 1) / NT;
+  T2 v[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NT;
     const int x = e / C, c = e - x * C;
     const int kz = kz0 + c;
-    T2 v{0, 0};
-    if (kz < a.nkz) v = in[(static_cast<long long>(y) * NX + x) * a.nkz + kz];
-    s[c * PITCH + x] = v;
+    v[q] = T2{0, 0};
+    if (e < NX * C && kz < a.nkz) v[q] = in[(static_cast<long long>(y) * NX + x) * a.nkz + kz];
+  }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + q * NT;
+    const int x = e / C, c = e - x * C;
+    if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
   }
   __syncthreads();
-  lds_fft<NX, C, NT, false>(s, PITCH, tw, tid);
+  lds_fft<NX, C, PITCH, NT, false>(s, tw, tid);
   T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
   for (int e = tid; e < a.nkx * C; e += NT) {
     const int i = e / C, c = e - i * C;
@@ -125,7 +154,7 @@ __global__ void __launch_bounds__(256) xfft_forward_kernel(XArgs a, const typena
       const int x = i <= a.Kx ? i : NX - (a.nkx - i);
       const int d = find_block(dst.kx_start, dst.ndst, i);
       const int nk = dst.kx_start[d + 1] - dst.kx_start[d];
-      outb[dst.off[d] + (static_cast<long long>(y) * nk + (i - dst.kx_start[d])) * a.nkz + kz] = s[c * PITCH + x];
+      outb[dst.off[d] + (static_cast<long long>(y) * nk + (i - dst.kx_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
     }
   }
 }
@@ -148,7 +177,7 @@ static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddle
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
     constexpr int C = XCfg<NN, T>::C;
-    dim3 grid(a.ny, (a.nkz + C - 1) / C, a.nfields);
+    dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
     hipLaunchKernelGGL((xfft_backward_kernel<NN, T>), grid, dim3(256), 0, s, a, src, static_cast<T2*>(phys),
                        static_cast<const T2*>(tw.buf));
   });
@@ -160,7 +189,7 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
     constexpr int C = XCfg<NN, T>::C;
-    dim3 grid(a.ny, (a.nkz + C - 1) / C, a.nfields);
+    dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
     hipLaunchKernelGGL((xfft_forward_kernel<NN, T>), grid, dim3(256), 0, s, a, static_cast<const T2*>(phys), dst,
                        static_cast<const T2*>(tw.buf));
   });
@@ -199,7 +228,8 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   constexpr int NR = Cfg::NR, NT = Cfg::NT;
   constexpr int E = NR * NZP / NT > 0 ? NR * NZP / NT : 1;
   static_assert(NR % 2 == 0, "NR must be even");
-  __shared__ T2 s[3 * NR * NZP];
+  constexpr int PITCH = FftPitch<NZP>::value;
+  __shared__ T2 s[3 * NR * PITCH];
   __shared__ float red[4][NT / 64];
   const int tid = threadIdx.x;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
@@ -207,30 +237,60 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   const int Kz = a.nkz - 1;
   const long long fs = a.field_stride;
 
-  // gather: pair p = (field 2p, field 2p+1) -> Z = A + i B with Hermitian extension in kz
-  for (int e = tid; e < 3 * NR * NZP; e += NT) {
-    const int q = e / (3 * NZP);
-    const int rem = e - q * 3 * NZP;
-    const int p = rem / NZP, k = rem - p * NZP;
-    const long long row = row0 + q;
-    T2 z{0, 0};
-    if (row < nrows) {
-      int kk = -1;
-      bool conj = false;
-      if (k <= Kz) kk = k;
-      else if (k >= NZP - Kz) { kk = NZP - k; conj = true; }
-      if (kk >= 0) {
-        const T2 A = fields[(2 * p) * fs + row * a.nkz + kk];
-        const T2 B = fields[(2 * p + 1) * fs + row * a.nkz + kk];
-        if (kk == 0) z = T2{A.x, B.x};
-        else if (!conj) z = T2{A.x - B.y, A.y + B.x};
-        else z = T2{A.x + B.y, B.x - A.y};
+  // gather, pass 1: each retained coefficient is loaded exactly once, all loads of a field issued
+  // before its LDS stores.  Field 2p of row q -> slots [0, Kz] of LDS row (q,p); field 2p+1 -> slot
+  // N-k (k >= 1) and N/2 (k = 0; the Nyquist slot, unused since Kz < N/2).  The rows of one field
+  // are contiguous, so element e covers (row0 + e / nkz, e % nkz): tracked incrementally.
+  {
+    constexpr int MAXE = (NR * (NZP / 2) + NT - 1) / NT;  // nkz <= NZP/2
+    const int tot = NR * a.nkz;
+    const long long nvalid = (nrows - row0 < NR ? nrows - row0 : NR) * a.nkz;
+    const int qr0 = tid / a.nkz, k0 = tid - qr0 * a.nkz;
+    const int dq = NT / a.nkz, dk = NT - dq * a.nkz;
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      const T2* src = fields + f * fs + row0 * a.nkz;
+      T2 v[MAXE];
+#pragma unroll
+      for (int q = 0; q < MAXE; ++q) {
+        const int e = tid + q * NT;
+        v[q] = (e < tot && e < nvalid) ? src[e] : T2{0, 0};
+      }
+      int qr = qr0, k = k0;
+      const int p = f >> 1;
+#pragma unroll
+      for (int q = 0; q < MAXE; ++q) {
+        const int e = tid + q * NT;
+        if (e < tot) {
+          const int slot = (f & 1) == 0 ? k : (k == 0 ? NZP / 2 : NZP - k);
+          s[(qr * 3 + p) * PITCH + fft_pidx(slot)] = v[q];
+        }
+        qr += dq;
+        k += dk;
+        if (k >= a.nkz) { k -= a.nkz; ++qr; }
       }
     }
-    s[(q * 3 + p) * NZP + k] = z;
   }
   __syncthreads();
-  lds_fft<NZP, 3 * NR, NT, true>(s, NZP, tw, tid);
+  // pass 2: Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k), zero padding in between
+  for (int e = tid; e < 3 * NR * (NZP / 2); e += NT) {
+    const int rr = e / (NZP / 2), k = e - rr * (NZP / 2);
+    T2* row = s + rr * PITCH;
+    if (k == 0) {
+      const T2 A = row[fft_pidx(0)], B = row[fft_pidx(NZP / 2)];
+      row[fft_pidx(0)] = T2{A.x, B.x};
+      row[fft_pidx(NZP / 2)] = T2{0, 0};
+    } else if (k <= Kz) {
+      const T2 A = row[fft_pidx(k)], B = row[fft_pidx(NZP - k)];
+      row[fft_pidx(k)] = T2{A.x - B.y, A.y + B.x};
+      row[fft_pidx(NZP - k)] = T2{A.x + B.y, B.x - A.y};
+    } else {
+      row[fft_pidx(k)] = T2{0, 0};
+      row[fft_pidx(NZP - k)] = T2{0, 0};
+    }
+  }
+  __syncthreads();
+  lds_fft<NZP, 3 * NR, PITCH, NT, true>(s, tw, tid);
 
   // H = u x omega, CFL maxima
   T hx[E], hy[E], hz[E];
@@ -239,7 +299,8 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   for (int b = 0; b < E; ++b) {
     const int e = tid + b * NT;
     const int q = e / NZP, n = e - q * NZP;
-    const T2 z0 = s[(q * 3 + 0) * NZP + n], z1 = s[(q * 3 + 1) * NZP + n], z2 = s[(q * 3 + 2) * NZP + n];
+    const int pn = fft_pidx(n);
+    const T2 z0 = s[(q * 3 + 0) * PITCH + pn], z1 = s[(q * 3 + 1) * PITCH + pn], z2 = s[(q * 3 + 2) * PITCH + pn];
     const T u = z0.x, v = z0.y, w = z1.x, wx = z1.y, wy = z2.x, wz = z2.y;
     hx[b] = v * wz - w * wy;
     hy[b] = w * wx - u * wz;
@@ -259,8 +320,9 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   for (int b = 0; b < E; ++b) {
     const int e = tid + b * NT;
     const int q = e / NZP, n = e - q * NZP;
-    s[q * NZP + n] = T2{hx[b], hy[b]};
-    reinterpret_cast<T*>(&s[(NR + q / 2) * NZP + n])[q & 1] = hz[b];
+    const int pn = fft_pidx(n);
+    s[q * PITCH + pn] = T2{hx[b], hy[b]};
+    reinterpret_cast<T*>(&s[(NR + q / 2) * PITCH + pn])[q & 1] = hz[b];
   }
   // block maxima
   for (int o = 32; o >= 1; o >>= 1) {
@@ -281,20 +343,22 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     for (int i = 0; i < NT / 64; ++i) m = fmaxf(m, red[tid][i]);
     atomic_max_pos(&a.maxima[tid], m);
   }
-  lds_fft<NZP, 3 * NR / 2, NT, false>(s, NZP, tw, tid);
+  lds_fft<NZP, 3 * NR / 2, PITCH, NT, false>(s, tw, tid);
 
   // extract retained kz, normalise, write H_x, H_y, H_z over fields 0..2
   const T sc = static_cast<T>(0.5 * a.scale);
-  for (int e = tid; e < NR * a.nkz; e += NT) {
-    const int q = e / a.nkz, k = e - q * a.nkz;
+  const int dq2 = NT / a.nkz, dk2 = NT - dq2 * a.nkz;
+  int q = tid / a.nkz, k = tid - q * a.nkz;
+  for (int e = tid; e < NR * a.nkz; e += NT, q += dq2, k += dk2) {
+    if (k >= a.nkz) { k -= a.nkz; ++q; }
     const long long row = row0 + q;
     if (row >= nrows) continue;
     const int km = (NZP - k) & (NZP - 1);
-    const T2 Z = s[q * NZP + k], Zm = s[q * NZP + km];
+    const T2 Z = s[q * PITCH + fft_pidx(k)], Zm = s[q * PITCH + fft_pidx(km)];
     // X = (Z + conj Zm)/2, Y = (Z - conj Zm)/(2i)
     const T2 X{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
     const T2 Y{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
-    const T2 P = s[(NR + q / 2) * NZP + k], Pm = s[(NR + q / 2) * NZP + km];
+    const T2 P = s[(NR + q / 2) * PITCH + fft_pidx(k)], Pm = s[(NR + q / 2) * PITCH + fft_pidx(km)];
     const T2 Hz = (q & 1) == 0 ? T2{(P.x + Pm.x) * sc, (P.y - Pm.y) * sc} : T2{(P.y + Pm.y) * sc, -(P.x - Pm.x) * sc};
     fields[0 * fs + row * a.nkz + k] = X;
     fields[1 * fs + row * a.nkz + k] = Y;
@@ -333,17 +397,18 @@ __global__ void __launch_bounds__(256) fft_test_kernel(typename C2<T>::type* dat
                                                        const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int ROWS = N >= 1024 ? 2 : 2048 / N;
-  __shared__ T2 s[ROWS * N];
+  constexpr int PITCH = FftPitch<N>::value;
+  __shared__ T2 s[ROWS * PITCH];
   const long long r0 = static_cast<long long>(blockIdx.x) * ROWS;
   for (int e = threadIdx.x; e < ROWS * N; e += 256) {
-    const int q = e / N;
-    s[e] = (r0 + q < batch) ? data[r0 * N + e] : T2{0, 0};
+    const int q = e / N, x = e - q * N;
+    s[q * PITCH + fft_pidx(x)] = (r0 + q < batch) ? data[r0 * N + e] : T2{0, 0};
   }
   __syncthreads();
-  lds_fft<N, ROWS, 256, INV>(s, N, tw, threadIdx.x);
+  lds_fft<N, ROWS, PITCH, 256, INV>(s, tw, threadIdx.x);
   for (int e = threadIdx.x; e < ROWS * N; e += 256) {
-    const int q = e / N;
-    if (r0 + q < batch) data[r0 * N + e] = s[e];
+    const int q = e / N, x = e - q * N;
+    if (r0 + q < batch) data[r0 * N + e] = s[q * PITCH + fft_pidx(x)];
   }
 }
 

@@ -21,6 +21,7 @@
 #include "channel/common.hpp"
 #include "channel/kernels.hpp"
 #include "channel/yline_device.hpp"
+#include "channel/fft_device.hpp"
 
 namespace channel {
 
@@ -88,9 +89,40 @@ void YTablesDev::upload(const YGrid& g, int R_, hipStream_t stream) {
   };
   std::vector<double> mask(N, 0.0);
   for (int j = 1; j < N - 1; ++j) mask[j] = 1.0;
+  // first and last rows of the dense D1 = A1^-1 B1: row_w = B1^T g, A1^T g = e_w (Thomas on A1^T)
+  auto d1_row = [&](int wall) {
+    std::vector<double> a(N, 0.0), b(N, 1.0), c(N, 0.0), d(N, 0.0);
+    for (int j = 0; j < N; ++j) {
+      a[j] = j > 0 ? g.d1_up[j - 1] : 0.0;      // (A1^T)[j][j-1] = A1[j-1][j]
+      c[j] = j < N - 1 ? g.d1_lo[j + 1] : 0.0;  // (A1^T)[j][j+1] = A1[j+1][j]
+    }
+    d[wall] = 1.0;
+    std::vector<double> cp(N), dp(N);
+    cp[0] = c[0] / b[0];
+    dp[0] = d[0] / b[0];
+    for (int j = 1; j < N; ++j) {
+      const double m = b[j] - a[j] * cp[j - 1];
+      cp[j] = c[j] / m;
+      dp[j] = (d[j] - a[j] * dp[j - 1]) / m;
+    }
+    std::vector<double> gv(N);
+    gv[N - 1] = dp[N - 1];
+    for (int j = N - 2; j >= 0; --j) gv[j] = dp[j] - cp[j] * gv[j + 1];
+    std::vector<double> row(N, 0.0);
+    for (int i = 1; i < N - 1; ++i) {
+      row[i - 1] += gv[i] * g.d1_rm[i];
+      row[i] += gv[i] * g.d1_rc[i];
+      row[i + 1] += gv[i] * g.d1_rp[i];
+    }
+    for (int k = 0; k < 3; ++k) {
+      row[k] += gv[0] * g.d1_w0[k];
+      row[N - 1 - k] += gv[N - 1] * g.d1_wN[k];
+    }
+    return row;
+  };
   std::vector<std::vector<double>> tabs = {lm(g.d1_lo), lm(g.d1_up), lm(g.d1_rm), lm(g.d1_rc), lm(g.d1_rp),
                                            lm(g.m_lo),  lm(g.m_up),  lm(g.k_lo),  lm(g.k_c),   lm(g.k_up),
-                                           lm(mask),    lm(g.trap)};
+                                           lm(mask),    lm(g.trap),  lm(d1_row(0)), lm(d1_row(N - 1))};
   int nf = 0;
   CH_DISPATCH_R(R, nf = PFac<R>::kNumFields);
   const size_t n = tabs.size() * rows + static_cast<size_t>(nf) * 64;
@@ -112,6 +144,8 @@ void YTablesDev::upload(const YGrid& g, int R_, hipStream_t stream) {
   tab.k_up = p + 9 * rows;
   tab.mask = p + 10 * rows;
   tab.trap = p + 11 * rows;
+  tab.d1row0 = p + 12 * rows;
+  tab.d1rowN = p + 13 * rows;
   double* fac = buf + tabs.size() * rows;
   tab.d1fac = fac;
   for (int i = 0; i < 3; ++i) {
@@ -249,23 +283,36 @@ template <int R, typename T, int W>
 struct SpecTile {
   using T2 = typename Cplx<T>::type;
   static constexpr int PITCH = W + 1;
+  // r-planes padded by one slot so consecutive y rows (consecutive r) of a staging store differ in bank
+  static constexpr int PLANE = 64 * PITCH + 1;
   T2* tile;
   int N, lines, line0, w, lane;
 
   __device__ void load(const T2* __restrict__ src, double (&x)[2][R]) const {
-    __syncthreads();
-    for (int e = threadIdx.x; e < N * W; e += W * 64) {
+    // all global loads of a thread in flight together (N*W <= 64*R*W => at most R per thread)
+    T2 v[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int e = threadIdx.x + q * W * 64;
       const int y = e / W, l = e - y * W;
-      T2 v{0, 0};
-      if (line0 + l < lines) v = src[static_cast<size_t>(y) * lines + line0 + l];
-      const int ly = y / R, r = y - ly * R;
-      tile[(r * 64 + ly) * PITCH + l] = v;
+      v[q] = T2{0, 0};
+      if (e < N * W && line0 + l < lines) v[q] = src[static_cast<size_t>(y) * lines + line0 + l];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int e = threadIdx.x + q * W * 64;
+      if (e < N * W) {
+        const int y = e / W, l = e - y * W;
+        const int ly = y / R, r = y - ly * R;
+        tile[r * PLANE + ly * PITCH + l] = v[q];
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = lane * R + r;
-      const T2 v = tile[(r * 64 + lane) * PITCH + w];
+      const T2 v = tile[r * PLANE + lane * PITCH + w];
       x[0][r] = j < N ? static_cast<double>(v.x) : 0.0;
       x[1][r] = j < N ? static_cast<double>(v.y) : 0.0;
     }
@@ -273,13 +320,13 @@ struct SpecTile {
   __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) const {
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; ++r) tile[(r * 64 + lane) * PITCH + w] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
+    for (int r = 0; r < R; ++r) tile[r * PLANE + lane * PITCH + w] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
     __syncthreads();
     for (int e = threadIdx.x; e < N * W; e += W * 64) {
       const int y = e / W, l = e - y * W;
       if (line0 + l < lines) {
         const int ly = y / R, r = y - ly * R;
-        dst[static_cast<size_t>(y) * lines + line0 + l] = tile[(r * 64 + ly) * PITCH + l];
+        dst[static_cast<size_t>(y) * lines + line0 + l] = tile[r * PLANE + ly * PITCH + l];
       }
     }
   }
@@ -294,14 +341,43 @@ __device__ __forceinline__ void czero(double (&x)[2][R]) {
 }
 
 template <int R, typename T, int W>
-__global__ void __launch_bounds__(W * 64) kspec_kernel(YTab t, SpecArgs a) {
+__global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
-  __shared__ T2 tile_mem[64 * R * (W + 1)];
+  // Coefficient tables (14 per-row tables + the D1 factorisation) are staged into LDS once per
+  // block when they fit: every solve step reads them, and from L2 each read is a dependent
+  // ~500-cycle load at one wave per SIMD.  Offsets are compile-time so the reads stay ds_read.
+  constexpr int ROWS = 64 * R;
+  constexpr int NTAB = 14 * ROWS + PFac<R>::kNumFields * 64;
+  constexpr bool TLDS = NTAB * 8 <= 72 * 1024;
+  __shared__ double tab_lds[TLDS ? NTAB : 1];
+  YTab t = tg;
+  if constexpr (TLDS) {
+    const double* src = tg.d1_lo;  // the table buffer is contiguous, d1_lo first (YTablesDev::upload)
+    for (int i = threadIdx.x; i < NTAB; i += W * 64) tab_lds[i] = src[i];
+    t.d1_lo = tab_lds + 0 * ROWS;
+    t.d1_up = tab_lds + 1 * ROWS;
+    t.d1_rm = tab_lds + 2 * ROWS;
+    t.d1_rc = tab_lds + 3 * ROWS;
+    t.d1_rp = tab_lds + 4 * ROWS;
+    t.m_lo = tab_lds + 5 * ROWS;
+    t.m_up = tab_lds + 6 * ROWS;
+    t.k_lo = tab_lds + 7 * ROWS;
+    t.k_c = tab_lds + 8 * ROWS;
+    t.k_up = tab_lds + 9 * ROWS;
+    t.mask = tab_lds + 10 * ROWS;
+    t.trap = tab_lds + 11 * ROWS;
+    t.d1row0 = tab_lds + 12 * ROWS;
+    t.d1rowN = tab_lds + 13 * ROWS;
+    t.d1fac = tab_lds + 14 * ROWS;
+    __syncthreads();
+  }
+  __shared__ T2 tile_mem[R * (64 * (W + 1) + 1)];
   double* sred = reinterpret_cast<double*>(tile_mem);  // stats reduction reuses the staging tile
   static_assert(sizeof(T2) * (W + 1) >= 4 * sizeof(double), "tile too small for the stats reduction");
   const int lane = __lane_id();
   const int w = threadIdx.x / 64;
-  const int line0 = blockIdx.x * W;
+  // XCD-aware tile order: tiles adjacent in memory (partial 128-B lines) land in one L2
+  const int line0 = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x)) * W;
   const int line = line0 + w;
   const bool valid = line < a.lines;
   const int N = a.N;
@@ -464,10 +540,6 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab t, SpecArgs a) {
       psolve<R, 2>(F, ci, phH, lane);
     }
     st.store(omega, rhsW);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int r = 0; r < R; ++r) om[k][r] = rhsW[k][r];
 
     // ---------------- velocity recovery + influence matrix (v(+-1) = v'(+-1) = 0) ----------
     {
@@ -479,23 +551,23 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab t, SpecArgs a) {
       psolve<R, 2>(F, chm, v, lane);
       apply_M<R, 2>(t, phH, vH, lane);
       psolve<R, 2>(F, chm, vH, lane);
-      double tmp[2][R];
+      // wall derivatives v'(+-1) = first / last row of the dense D1 applied to v (no solves)
+      double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int r = 0; r < R; ++r) tmp[k][r] = v[k][r];
-      d1_apply<R, 2>(t, tmp, lane);
-      double p0r, p0i, pNr, pNi;
-      row_cplx<R>(tmp, 0, lane, p0r, p0i);
-      row_cplx<R>(tmp, N - 1, lane, pNr, pNi);
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int r = 0; r < R; ++r) tmp[k][r] = vH[k][r];
-      d1_apply<R, 2>(t, tmp, lane);
-      // homogeneous wall derivatives: tmp[0] = dv_h1 (phi(-1)=1), tmp[1] = dv_h2 (phi(+1)=1)
-      const double h10 = row_value<R>(tmp[0], 0, lane), h1N = row_value<R>(tmp[0], N - 1, lane);
-      const double h20 = row_value<R>(tmp[1], 0, lane), h2N = row_value<R>(tmp[1], N - 1, lane);
+      for (int r = 0; r < R; ++r) {
+        const double g0 = tab(t.d1row0, r, lane), gN = tab(t.d1rowN, r, lane);
+        acc[0] += g0 * v[0][r];
+        acc[1] += g0 * v[1][r];
+        acc[2] += gN * v[0][r];
+        acc[3] += gN * v[1][r];
+        acc[4] += g0 * vH[0][r];
+        acc[5] += gN * vH[0][r];
+        acc[6] += g0 * vH[1][r];
+        acc[7] += gN * vH[1][r];
+      }
+      wave_sum_n<8>(acc);
+      const double p0r = acc[0], p0i = acc[1], pNr = acc[2], pNi = acc[3];
+      const double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
       const double det = h10 * h2N - h20 * h1N;
       const bool apply = !is_mean && k2 > 0.0 && dt > 1e-14 && det != 0.0;
       const double id = apply ? 1.0 / det : 0.0;
@@ -515,6 +587,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab t, SpecArgs a) {
       }
     }
     st.store(phi, ph);
+    st.load(omega, om);  // reload (cheaper than keeping 2R doubles live through the influence step)
   } else {
     // ---------------- prepare only: fields from the state ----------------------------------
     st.load(phi, ph);
