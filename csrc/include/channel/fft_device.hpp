@@ -208,6 +208,62 @@ __device__ void lds_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int tid
   if constexpr (Pl::R2 > 1) stockham_pass<N, Pl::R2, Pl::R0 * Pl::R1, ROWS, PITCH, NT, INV>(buf, tw, tid);
 }
 
+// ---- wave-owned variant -------------------------------------------------------------------
+// One wavefront transforms RW rows it owns.  A wave's LDS instructions are processed in order,
+// so the pass structure (all reads of a pass, then all writes) needs no s_barrier: the only
+// requirement is that the compiler keeps the program order of the (possibly aliasing) LDS
+// accesses, which wave_barrier() pins.  Blocks then need barriers only around cooperative
+// global<->LDS staging, not per pass.
+template <int N, int R, int NS, int RW, int PITCH, bool INV, typename T2>
+__device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
+  constexpr int Q = N / R;
+  constexpr int NB = RW * Q;
+  constexpr int B = (NB + 63) / 64;
+  T2 v[B][R];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int idx = lane + b * 64;
+    if (NB % 64 == 0 || idx < NB) {
+      const int row = idx / Q, j = idx - row * Q;
+      const T2* p = buf + row * PITCH;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(j + r * Q)];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int idx = lane + b * 64;
+    if (NB % 64 == 0 || idx < NB) {
+      const int row = idx / Q, j = idx - row * Q;
+      const int k = j & (NS - 1);
+      if constexpr (NS > 1) {
+        constexpr int stride = N / (R * NS);
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          T2 w = tw[k * r * stride];
+          if (INV) w.y = -w.y;
+          v[b][r] = cmul(v[b][r], w);
+        }
+      }
+      dftR<R, INV>(v[b]);
+      T2* p = buf + row * PITCH;
+      const int base = (j - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) p[fft_pidx(base + r * NS)] = v[b][r];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int N, int RW, int PITCH, bool INV, typename T2>
+__device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
+  using Pl = FftPlan<N>;
+  wave_pass<N, Pl::R0, 1, RW, PITCH, INV>(buf, tw, lane);
+  if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV>(buf, tw, lane);
+  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw, lane);
+}
+
 // XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so logical tiles that are adjacent in memory are given to blocks
 // on the same XCD (their partial cache lines then merge in one L2).  Bijective for any n.

@@ -105,7 +105,11 @@ __global__ void __launch_bounds__(256) xfft_backward_kernel(XArgs a, XSrc src, t
     if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
   }
   __syncthreads();
-  lds_fft<NX, C, PITCH, NT, true>(s, tw, tid);
+  {
+    constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
+    wave_fft<NX, RW, PITCH, true>(s + (tid / 64) * RW * PITCH, tw, tid & 63);
+  }
+  __syncthreads();
   T2* out = phys + f * a.field_stride_phys;
   for (int e = tid; e < NX * C; e += NT) {
     const int x = e / C, c = e - x * C;
@@ -145,7 +149,11 @@ __global__ void __launch_bounds__(256) xfft_forward_kernel(XArgs a, const typena
     if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
   }
   __syncthreads();
-  lds_fft<NX, C, PITCH, NT, false>(s, tw, tid);
+  {
+    constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
+    wave_fft<NX, RW, PITCH, false>(s + (tid / 64) * RW * PITCH, tw, tid & 63);
+  }
+  __syncthreads();
   T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
   for (int e = tid; e < a.nkx * C; e += NT) {
     const int i = e / C, c = e - i * C;
@@ -210,159 +218,126 @@ void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twidd
 }
 
 // ---- z-direction physical stage -------------------------------------------------------------
-template <int NZP, typename T>
-struct ZCfg {
-  static constexpr int NR = sizeof(T) == 4 ? (2048 / NZP > 2 ? 2048 / NZP : 2) : (1024 / NZP > 2 ? 1024 / NZP : 2);
-  static constexpr int NT = 256;
-};
-
 __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
   atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
 }
+
+// One wave per (y,x) row; a block holds ZW rows and each wave owns one LDS row buffer, so there is
+// no block barrier between the gather, the five FFTs, the product and the extraction.  The six
+// physical fields stay in registers (each lane owns points n = lane + 64 i of the row).
+constexpr int ZW = 4;
 
 template <int NZP, typename T>
 __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                     const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
-  using Cfg = ZCfg<NZP, T>;
-  constexpr int NR = Cfg::NR, NT = Cfg::NT;
-  constexpr int E = NR * NZP / NT > 0 ? NR * NZP / NT : 1;
-  static_assert(NR % 2 == 0, "NR must be even");
   constexpr int PITCH = FftPitch<NZP>::value;
-  __shared__ T2 s[3 * NR * PITCH];
-  __shared__ float red[4][NT / 64];
-  const int tid = threadIdx.x;
+  constexpr int EP = (NZP + 63) / 64;  // points per lane
+  __shared__ T2 s[ZW * PITCH];
+  __shared__ float red[4][ZW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
-  const long long row0 = static_cast<long long>(blockIdx.x) * NR;
-  const int Kz = a.nkz - 1;
+  const long long r = static_cast<long long>(blockIdx.x) * ZW + w;
+  const int Kz = a.nkz - 1, nkz = a.nkz;
   const long long fs = a.field_stride;
-
-  // gather, pass 1: each retained coefficient is loaded exactly once, all loads of a field issued
-  // before its LDS stores.  Field 2p of row q -> slots [0, Kz] of LDS row (q,p); field 2p+1 -> slot
-  // N-k (k >= 1) and N/2 (k = 0; the Nyquist slot, unused since Kz < N/2).  The rows of one field
-  // are contiguous, so element e covers (row0 + e / nkz, e % nkz): tracked incrementally.
-  {
-    constexpr int MAXE = (NR * (NZP / 2) + NT - 1) / NT;  // nkz <= NZP/2
-    const int tot = NR * a.nkz;
-    const long long nvalid = (nrows - row0 < NR ? nrows - row0 : NR) * a.nkz;
-    const int qr0 = tid / a.nkz, k0 = tid - qr0 * a.nkz;
-    const int dq = NT / a.nkz, dk = NT - dq * a.nkz;
-#pragma unroll
-    for (int f = 0; f < 6; ++f) {
-      const T2* src = fields + f * fs + row0 * a.nkz;
-      T2 v[MAXE];
-#pragma unroll
-      for (int q = 0; q < MAXE; ++q) {
-        const int e = tid + q * NT;
-        v[q] = (e < tot && e < nvalid) ? src[e] : T2{0, 0};
-      }
-      int qr = qr0, k = k0;
-      const int p = f >> 1;
-#pragma unroll
-      for (int q = 0; q < MAXE; ++q) {
-        const int e = tid + q * NT;
-        if (e < tot) {
-          const int slot = (f & 1) == 0 ? k : (k == 0 ? NZP / 2 : NZP - k);
-          s[(qr * 3 + p) * PITCH + fft_pidx(slot)] = v[q];
-        }
-        qr += dq;
-        k += dk;
-        if (k >= a.nkz) { k -= a.nkz; ++qr; }
-      }
-    }
-  }
-  __syncthreads();
-  // pass 2: Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k), zero padding in between
-  for (int e = tid; e < 3 * NR * (NZP / 2); e += NT) {
-    const int rr = e / (NZP / 2), k = e - rr * (NZP / 2);
-    T2* row = s + rr * PITCH;
-    if (k == 0) {
-      const T2 A = row[fft_pidx(0)], B = row[fft_pidx(NZP / 2)];
-      row[fft_pidx(0)] = T2{A.x, B.x};
-      row[fft_pidx(NZP / 2)] = T2{0, 0};
-    } else if (k <= Kz) {
-      const T2 A = row[fft_pidx(k)], B = row[fft_pidx(NZP - k)];
-      row[fft_pidx(k)] = T2{A.x - B.y, A.y + B.x};
-      row[fft_pidx(NZP - k)] = T2{A.x + B.y, B.x - A.y};
-    } else {
-      row[fft_pidx(k)] = T2{0, 0};
-      row[fft_pidx(NZP - k)] = T2{0, 0};
-    }
-  }
-  __syncthreads();
-  lds_fft<NZP, 3 * NR, PITCH, NT, true>(s, tw, tid);
-
-  // H = u x omega, CFL maxima
-  T hx[E], hy[E], hz[E];
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
+
+  if (r < nrows) {  // wave-uniform
+    T2 ph[3][EP];
 #pragma unroll
-  for (int b = 0; b < E; ++b) {
-    const int e = tid + b * NT;
-    const int q = e / NZP, n = e - q * NZP;
-    const int pn = fft_pidx(n);
-    const T2 z0 = s[(q * 3 + 0) * PITCH + pn], z1 = s[(q * 3 + 1) * PITCH + pn], z2 = s[(q * 3 + 2) * PITCH + pn];
-    const T u = z0.x, v = z0.y, w = z1.x, wx = z1.y, wy = z2.x, wz = z2.y;
-    hx[b] = v * wz - w * wy;
-    hy[b] = w * wx - u * wz;
-    hz[b] = u * wy - v * wx;
-    const long long row = row0 + q;
-    if (row < nrows) {
-      const int yl = static_cast<int>(row / a.NX);
-      const float au = fabsf(static_cast<float>(u)), av = fabsf(static_cast<float>(v)), aw = fabsf(static_cast<float>(w));
+    for (int p = 0; p < 3; ++p) {
+      // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
+      // (a real z-row has a real mean), zero padding between Kz and N-Kz.
+      const T2* A = fields + (2 * p) * fs + r * nkz;
+      const T2* B = fields + (2 * p + 1) * fs + r * nkz;
+      constexpr int MK = (NZP / 2 + 63) / 64;
+      T2 va[MK], vb[MK];
+#pragma unroll
+      for (int i = 0; i < MK; ++i) {
+        const int k = lane + 64 * i;
+        va[i] = k < nkz ? A[k] : T2{0, 0};
+        vb[i] = k < nkz ? B[k] : T2{0, 0};
+      }
+#pragma unroll
+      for (int i = 0; i < MK; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          if (k == 0) {
+            row[fft_pidx(0)] = T2{va[i].x, vb[i].x};
+          } else {
+            row[fft_pidx(k)] = T2{va[i].x - vb[i].y, va[i].y + vb[i].x};
+            row[fft_pidx(NZP - k)] = T2{va[i].x + vb[i].y, vb[i].x - va[i].y};
+          }
+        }
+      }
+      for (int k = Kz + 1 + lane; k < NZP - Kz; k += 64) row[fft_pidx(k)] = T2{0, 0};
+      __builtin_amdgcn_wave_barrier();
+      wave_fft<NZP, 1, PITCH, true>(row, tw, lane);
+#pragma unroll
+      for (int i = 0; i < EP; ++i) {
+        const int n = lane + 64 * i;
+        ph[p][i] = n < NZP ? row[fft_pidx(n)] : T2{0, 0};
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
+    const int yl = static_cast<int>(r / a.NX);
+    const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    T hz[EP];
+#pragma unroll
+    for (int i = 0; i < EP; ++i) {
+      const T u = ph[0][i].x, v = ph[0][i].y, ww = ph[1][i].x, wx = ph[1][i].y, wy = ph[2][i].x, wz = ph[2][i].y;
+      const T hx = v * wz - ww * wy, hy = ww * wx - u * wz;
+      hz[i] = u * wy - v * wx;
+      const float au = fabsf(static_cast<float>(u)), av = fabsf(static_cast<float>(v)), aw = fabsf(static_cast<float>(ww));
       mu = fmaxf(mu, au);
       mv = fmaxf(mv, av);
       mw = fmaxf(mw, aw);
-      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * a.inv_dy[a.y0 + yl] + aw * a.cz));
+      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+      const int n = lane + 64 * i;
+      if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
+    }
+    __builtin_amdgcn_wave_barrier();
+    const T sc = static_cast<T>(0.5 * a.scale);
+    wave_fft<NZP, 1, PITCH, false>(row, tw, lane);
+    // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
+    for (int k = lane; k < nkz; k += 64) {
+      const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
+      fields[0 * fs + r * nkz + k] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+      fields[1 * fs + r * nkz + k] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < EP; ++i) {
+      const int n = lane + 64 * i;
+      if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
+    }
+    __builtin_amdgcn_wave_barrier();
+    wave_fft<NZP, 1, PITCH, false>(row, tw, lane);
+    for (int k = lane; k < nkz; k += 64) {
+      const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
+      fields[2 * fs + r * nkz + k] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < E; ++b) {
-    const int e = tid + b * NT;
-    const int q = e / NZP, n = e - q * NZP;
-    const int pn = fft_pidx(n);
-    s[q * PITCH + pn] = T2{hx[b], hy[b]};
-    reinterpret_cast<T*>(&s[(NR + q / 2) * PITCH + pn])[q & 1] = hz[b];
-  }
-  // block maxima
+  // block maxima -> one atomicMax per block and quantity
   for (int o = 32; o >= 1; o >>= 1) {
     mu = fmaxf(mu, __shfl_xor(mu, o));
     mv = fmaxf(mv, __shfl_xor(mv, o));
     mw = fmaxf(mw, __shfl_xor(mw, o));
     mc = fmaxf(mc, __shfl_xor(mc, o));
   }
-  if ((tid & 63) == 0) {
-    red[0][tid / 64] = mu;
-    red[1][tid / 64] = mv;
-    red[2][tid / 64] = mw;
-    red[3][tid / 64] = mc;
+  if (lane == 0) {
+    red[0][w] = mu;
+    red[1][w] = mv;
+    red[2][w] = mw;
+    red[3][w] = mc;
   }
   __syncthreads();
   if (tid < 4 && a.maxima) {
     float m = 0.f;
-    for (int i = 0; i < NT / 64; ++i) m = fmaxf(m, red[tid][i]);
+    for (int i = 0; i < ZW; ++i) m = fmaxf(m, red[tid][i]);
     atomic_max_pos(&a.maxima[tid], m);
-  }
-  lds_fft<NZP, 3 * NR / 2, PITCH, NT, false>(s, tw, tid);
-
-  // extract retained kz, normalise, write H_x, H_y, H_z over fields 0..2
-  const T sc = static_cast<T>(0.5 * a.scale);
-  const int dq2 = NT / a.nkz, dk2 = NT - dq2 * a.nkz;
-  int q = tid / a.nkz, k = tid - q * a.nkz;
-  for (int e = tid; e < NR * a.nkz; e += NT, q += dq2, k += dk2) {
-    if (k >= a.nkz) { k -= a.nkz; ++q; }
-    const long long row = row0 + q;
-    if (row >= nrows) continue;
-    const int km = (NZP - k) & (NZP - 1);
-    const T2 Z = s[q * PITCH + fft_pidx(k)], Zm = s[q * PITCH + fft_pidx(km)];
-    // X = (Z + conj Zm)/2, Y = (Z - conj Zm)/(2i)
-    const T2 X{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
-    const T2 Y{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
-    const T2 P = s[(NR + q / 2) * PITCH + fft_pidx(k)], Pm = s[(NR + q / 2) * PITCH + fft_pidx(km)];
-    const T2 Hz = (q & 1) == 0 ? T2{(P.x + Pm.x) * sc, (P.y - Pm.y) * sc} : T2{(P.y + Pm.y) * sc, -(P.x - Pm.x) * sc};
-    fields[0 * fs + row * a.nkz + k] = X;
-    fields[1 * fs + row * a.nkz + k] = Y;
-    fields[2 * fs + row * a.nkz + k] = Hz;
   }
 }
 
@@ -373,9 +348,8 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
     if constexpr (sizeof(T) == 8 && NN > 1024) {
       CH_CHECK(false, "fp64 storage supports 2NZ-2 <= 1024");
     } else {
-      constexpr int NR = ZCfg<NN, T>::NR;
       const long long nrows = static_cast<long long>(a.ny) * a.NX;
-      dim3 grid(static_cast<unsigned>((nrows + NR - 1) / NR));
+      dim3 grid(static_cast<unsigned>((nrows + ZW - 1) / ZW));
       hipLaunchKernelGGL((zphys_kernel<NN, T>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
                          static_cast<const T2*>(tw.buf));
     }
@@ -396,31 +370,26 @@ template <int N, typename T, bool INV>
 __global__ void __launch_bounds__(256) fft_test_kernel(typename C2<T>::type* data, int batch,
                                                        const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
-  constexpr int ROWS = N >= 1024 ? 2 : 2048 / N;
   constexpr int PITCH = FftPitch<N>::value;
-  __shared__ T2 s[ROWS * PITCH];
-  const long long r0 = static_cast<long long>(blockIdx.x) * ROWS;
-  for (int e = threadIdx.x; e < ROWS * N; e += 256) {
-    const int q = e / N, x = e - q * N;
-    s[q * PITCH + fft_pidx(x)] = (r0 + q < batch) ? data[r0 * N + e] : T2{0, 0};
-  }
-  __syncthreads();
-  lds_fft<N, ROWS, PITCH, 256, INV>(s, tw, threadIdx.x);
-  for (int e = threadIdx.x; e < ROWS * N; e += 256) {
-    const int q = e / N, x = e - q * N;
-    if (r0 + q < batch) data[r0 * N + e] = s[q * PITCH + fft_pidx(x)];
-  }
+  __shared__ T2 s[4 * PITCH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long rw = static_cast<long long>(blockIdx.x) * 4 + w;
+  if (rw >= batch) return;  // wave-uniform; no block barriers below
+  T2* row = s + w * PITCH;
+  for (int x = lane; x < N; x += 64) row[fft_pidx(x)] = data[rw * N + x];
+  __builtin_amdgcn_wave_barrier();
+  wave_fft<N, 1, PITCH, INV>(row, tw, lane);
+  for (int x = lane; x < N; x += 64) data[rw * N + x] = row[fft_pidx(x)];
 }
 
 template <typename T>
 static void fft_test_launch(void* data, int n, int batch, int dir, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(n, {
-    constexpr int ROWS = NN >= 1024 ? 2 : 2048 / NN;
     if constexpr (sizeof(T) == 8 && NN > 1024) {
       CH_CHECK(false, "fp64 test FFT supports n <= 1024");
     } else {
-      dim3 grid((batch + ROWS - 1) / ROWS);
+      dim3 grid((batch + 3) / 4);
       if (dir > 0)
         hipLaunchKernelGGL((fft_test_kernel<NN, T, true>), grid, dim3(256), 0, s, static_cast<T2*>(data), batch,
                            static_cast<const T2*>(tw.buf));
