@@ -153,8 +153,34 @@ def op_K(ops: YOps, x: np.ndarray) -> np.ndarray:
 
 
 def _bsolve(A: np.ndarray, rhs: np.ndarray) -> np.ndarray:
-    # A [L, N, N], rhs [N, L] -> [N, L]
-    return np.linalg.solve(A, rhs.T[..., None])[..., 0].T
+    # A [L, N, N] (tridiagonal), rhs [N, L] -> [N, L]; vectorised Thomas over the L lines
+    N = A.shape[-1]
+    idx = np.arange(N)
+    d = A[:, idx, idx].T.copy()                       # [N, L]
+    lo = np.zeros_like(d)
+    up = np.zeros_like(d)
+    lo[1:] = A[:, idx[1:], idx[:-1]].T
+    up[:-1] = A[:, idx[:-1], idx[1:]].T
+    return tri_solve(lo, d, up, rhs)
+
+
+def tri_solve(lo: np.ndarray, d: np.ndarray, up: np.ndarray, rhs: np.ndarray) -> np.ndarray:
+    """Thomas algorithm on [N, L] coefficient/RHS arrays (vectorised over the L lines)."""
+    N = d.shape[0]
+    rhs = np.asarray(rhs)
+    cp = np.empty_like(d)
+    dp = np.empty(rhs.shape, dtype=np.result_type(rhs, d))
+    cp[0] = up[0] / d[0]
+    dp[0] = rhs[0] / d[0]
+    for j in range(1, N):
+        m = d[j] - lo[j] * cp[j - 1]
+        cp[j] = up[j] / m
+        dp[j] = (rhs[j] - lo[j] * dp[j - 1]) / m
+    x = np.empty_like(dp)
+    x[-1] = dp[-1]
+    for j in range(N - 2, -1, -1):
+        x[j] = dp[j] - cp[j] * x[j + 1]
+    return x
 
 
 def op_helm(ops: YOps, x: np.ndarray, k2: np.ndarray) -> np.ndarray:
@@ -329,12 +355,12 @@ class OracleSolver:
         import torch
         import torch.distributed as dist
 
-        P = self.plan.P
         send = [torch.from_numpy(np.ascontiguousarray(b).view(np.float64)).reshape(-1) for b in blocks_send]
-        recv_sizes = self._recv_sizes
-        recv = [torch.empty(s, dtype=torch.float64) for s in recv_sizes]
-        dist.all_to_all(recv, send, group=self.dist)
-        return [r.numpy() for r in recv]
+        in_splits = [t.numel() for t in send]
+        out_splits = list(self._recv_sizes)
+        out = torch.empty(sum(out_splits), dtype=torch.float64)
+        dist.all_to_all_single(out, torch.cat(send), out_splits, in_splits, group=self.dist)
+        return [t.numpy() for t in torch.split(out, out_splits)]
 
     def transforms(self, compute_dt: bool):
         p = self.plan

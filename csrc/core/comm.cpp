@@ -1,8 +1,16 @@
 #include "channel/comm.hpp"
 
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "channel/common.hpp"
 
@@ -20,7 +28,15 @@ std::string Comm::new_unique_id() {
   return std::string(id.internal, id.internal + sizeof(id.internal));
 }
 
-Comm::Comm(int rank, int nranks, const std::string& uid, int device) : rank_(rank), size_(nranks) {
+std::unique_ptr<Comm> Comm::create(int rank, int nranks, const std::string& uid, int device) {
+  if (uid.rfind("shm:", 0) == 0) return std::make_unique<ShmComm>(rank, nranks, uid.substr(4));
+  return std::make_unique<RcclComm>(rank, nranks, uid, device);
+}
+
+// ---- RCCL --------------------------------------------------------------------------------------
+RcclComm::RcclComm(int rank, int nranks, const std::string& uid, int device) {
+  rank_ = rank;
+  size_ = nranks;
   CH_CHECK(uid.size() == sizeof(ncclUniqueId::internal), "bad ncclUniqueId size " << uid.size());
   HIP_CHECK(hipSetDevice(device));
   ncclUniqueId id;
@@ -30,17 +46,18 @@ Comm::Comm(int rank, int nranks, const std::string& uid, int device) : rank_(ran
   comm_ = c;
 }
 
-Comm::~Comm() {
+RcclComm::~RcclComm() {
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
 }
 
-void Comm::abort() {
+void RcclComm::abort() {
   if (comm_) ncclCommAbort(static_cast<ncclComm_t>(comm_));
   comm_ = nullptr;
 }
 
-void Comm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
-                     const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) {
+void RcclComm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
+                         void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
+                         hipStream_t s) {
   auto c = static_cast<ncclComm_t>(comm_);
   const char* sb = static_cast<const char*>(send);
   char* rb = static_cast<char*>(recv);
@@ -52,17 +69,140 @@ void Comm::alltoallv(const void* send, const std::vector<size_t>& scount, const 
   NCCL_CHECK(ncclGroupEnd());
 }
 
-void Comm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
+void RcclComm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclFloat, ncclMax, static_cast<ncclComm_t>(comm_), s));
 }
-void Comm::allreduce_sum_f64(double* buf, size_t n, hipStream_t s) {
+void RcclComm::allreduce_sum_f64(double* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
-void Comm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
+void RcclComm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, static_cast<ncclComm_t>(comm_), s));
 }
-void Comm::broadcast(void* buf, size_t bytes, int root, hipStream_t s) {
-  NCCL_CHECK(ncclBroadcast(buf, buf, bytes, ncclChar, root, static_cast<ncclComm_t>(comm_), s));
+
+// ---- shared-memory loopback (tests) -----------------------------------------------------------
+namespace {
+struct ShmHeader {
+  std::atomic<int> ready;
+  std::atomic<int> count;
+  std::atomic<int> sense;
+  int nranks;
+  size_t slot_bytes;
+};
+constexpr size_t kHdr = 4096;
+}  // namespace
+
+ShmComm::ShmComm(int rank, int nranks, const std::string& name) : name_("/" + name) {
+  rank_ = rank;
+  size_ = nranks;
+  const char* mb = std::getenv("CHANNEL_SHM_SLOT_MB");
+  slot_bytes_ = static_cast<size_t>(mb ? std::atoi(mb) : 16) << 20;
+  bytes_ = kHdr + static_cast<size_t>(nranks) * nranks * slot_bytes_;
+  int fd = -1;
+  if (rank == 0) {
+    shm_unlink(name_.c_str());
+    fd = shm_open(name_.c_str(), O_CREAT | O_RDWR, 0600);
+    CH_CHECK(fd >= 0, "shm_open(" << name_ << ") failed");
+    CH_CHECK(ftruncate(fd, static_cast<off_t>(bytes_)) == 0, "ftruncate shm failed");
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((fd = shm_open(name_.c_str(), O_RDWR, 0600)) < 0) {
+      CH_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(120), "timeout waiting for shm " << name_);
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    struct stat st;
+    do {
+      fstat(fd, &st);
+    } while (static_cast<size_t>(st.st_size) < bytes_);
+  }
+  base_ = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  CH_CHECK(base_ != MAP_FAILED, "mmap shm failed");
+  auto* h = static_cast<ShmHeader*>(base_);
+  if (rank == 0) {
+    h->count.store(0);
+    h->sense.store(0);
+    h->nranks = nranks;
+    h->slot_bytes = slot_bytes_;
+    h->ready.store(0x5eed);
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (h->ready.load() != 0x5eed) {
+      CH_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(120), "timeout waiting for shm init");
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+  }
+  barrier();
+}
+
+ShmComm::~ShmComm() {
+  try {
+    barrier();
+  } catch (...) {
+  }
+  if (base_) munmap(base_, bytes_);
+  if (rank_ == 0) shm_unlink(name_.c_str());
+}
+
+void ShmComm::barrier() {
+  auto* h = static_cast<ShmHeader*>(base_);
+  const int my_sense = 1 - h->sense.load();
+  if (h->count.fetch_add(1) == size_ - 1) {
+    h->count.store(0);
+    h->sense.store(my_sense);
+  } else {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (h->sense.load() != my_sense) {
+      CH_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(300), "ShmComm barrier timeout");
+      std::this_thread::yield();
+    }
+  }
+}
+
+char* ShmComm::slot(int src, int dst) {
+  return static_cast<char*>(base_) + kHdr + (static_cast<size_t>(src) * size_ + dst) * slot_bytes_;
+}
+
+void ShmComm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
+                        void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
+                        hipStream_t s) {
+  HIP_CHECK(hipStreamSynchronize(s));
+  for (int p = 0; p < size_; ++p) {
+    CH_CHECK(scount[p] <= slot_bytes_ && rcount[p] <= slot_bytes_,
+             "ShmComm slot too small (" << scount[p] << " bytes); set CHANNEL_SHM_SLOT_MB");
+    if (scount[p])
+      HIP_CHECK(hipMemcpy(slot(rank_, p), static_cast<const char*>(send) + soff[p], scount[p], hipMemcpyDeviceToHost));
+  }
+  barrier();
+  for (int p = 0; p < size_; ++p)
+    if (rcount[p])
+      HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + roff[p], slot(p, rank_), rcount[p], hipMemcpyHostToDevice));
+  barrier();
+}
+
+template <typename T, typename Op>
+void ShmComm::allreduce(T* buf, size_t n, hipStream_t s, Op op) {
+  HIP_CHECK(hipStreamSynchronize(s));
+  CH_CHECK(n * sizeof(T) <= slot_bytes_, "ShmComm allreduce too large");
+  HIP_CHECK(hipMemcpy(slot(rank_, 0), buf, n * sizeof(T), hipMemcpyDeviceToHost));
+  barrier();
+  std::vector<T> acc(n);
+  std::memcpy(acc.data(), slot(0, 0), n * sizeof(T));
+  for (int p = 1; p < size_; ++p) {
+    const T* v = reinterpret_cast<const T*>(slot(p, 0));
+    for (size_t i = 0; i < n; ++i) acc[i] = op(acc[i], v[i]);
+  }
+  barrier();
+  HIP_CHECK(hipMemcpy(buf, acc.data(), n * sizeof(T), hipMemcpyHostToDevice));
+}
+
+void ShmComm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
+  allreduce(buf, n, s, [](float a, float b) { return a > b ? a : b; });
+}
+void ShmComm::allreduce_sum_f64(double* buf, size_t n, hipStream_t s) {
+  allreduce(buf, n, s, [](double a, double b) { return a + b; });
+}
+void ShmComm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
+  allreduce(buf, n, s, [](unsigned a, unsigned b) { return a > b ? a : b; });
 }
 
 }  // namespace channel

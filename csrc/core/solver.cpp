@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <iostream>
@@ -64,7 +65,11 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
   HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
   if (nranks > 1) {
     CH_CHECK(!nccl_uid.empty(), "P > 1 requires an RCCL unique id");
-    comm_ = std::make_unique<Comm>(rank, nranks, nccl_uid, device_);
+    comm_ = Comm::create(rank, nranks, nccl_uid, device_);
+    // Multi-rank steps run eagerly by default (~100 launches per RK3 step, negligible at these
+    // grid sizes); capturing RCCL into the step graph is opt-in (CHANNEL_GRAPH_MULTI=1).
+    const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
+    if (!comm_->graph_capturable() || !(gm && std::atoi(gm) == 1)) use_graph_ = false;
     CH_CHECK(nranks <= 8, "slab decomposition supports P <= 8 ranks per job in this version");
   }
   ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);

@@ -1,14 +1,20 @@
-// RCCL communicator wrapper (one process per GPU, device-direct collectives over xGMI).
+// Communicators for the slab decomposition (one process per GPU).
 //
-// Replaces the reference's host-staged MPI_Alltoall transposes (channel_cuda_mpi.c:64-128: D2H copy,
-// MPI_Alltoall of pageable buffers, H2D copy, per-item cublasCgeam) and its scalar MPI_Allreduce
-// reductions (hit_mpi.c:427-455).  Bootstrap: the 128-byte ncclUniqueId is exchanged by the caller
-// (torch.distributed broadcast in Python, MPI_Bcast in the C++ driver).
+//  * RcclComm: device-direct RCCL collectives over xGMI (the production path).  Replaces the
+//    reference's host-staged MPI_Alltoall transposes (channel_cuda_mpi.c:64-128: D2H copy,
+//    MPI_Alltoall of pageable buffers, H2D copy, per-item cublasCgeam) and its scalar
+//    MPI_Allreduce reductions (hit_mpi.c:427-455).  Bootstrap: the 128-byte ncclUniqueId is
+//    exchanged by the caller (torch.distributed broadcast in Python, MPI_Bcast in the C++ driver).
+//  * ShmComm: host shared-memory loopback for testing P ranks that share one GPU (RCCL refuses
+//    two ranks on one device).  Synchronous and host-staged, so it is never captured in a graph;
+//    it exercises exactly the same send/recv block addressing as RcclComm.  Selected by a
+//    "shm:<name>" unique id.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -16,27 +22,64 @@ namespace channel {
 
 class Comm {
  public:
-  static std::string new_unique_id();  // 128 raw bytes
-  Comm(int rank, int nranks, const std::string& uid, int device);
-  ~Comm();
-  Comm(const Comm&) = delete;
-  Comm& operator=(const Comm&) = delete;
-
+  virtual ~Comm() = default;
   int rank() const { return rank_; }
   int size() const { return size_; }
+  virtual bool graph_capturable() const = 0;
 
   // variable all-to-all; counts/offsets in bytes (multiples of 4)
+  virtual void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
+                         void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
+                         hipStream_t s) = 0;
+  virtual void allreduce_max_f32(float* buf, size_t n, hipStream_t s) = 0;
+  virtual void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) = 0;
+  virtual void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) = 0;
+  virtual void abort() = 0;
+
+  static std::string new_unique_id();  // 128 raw bytes (RCCL)
+  // "shm:<name>" -> ShmComm, otherwise an RCCL unique id
+  static std::unique_ptr<Comm> create(int rank, int nranks, const std::string& uid, int device);
+
+ protected:
+  int rank_ = 0, size_ = 1;
+};
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(int rank, int nranks, const std::string& uid, int device);
+  ~RcclComm() override;
+  bool graph_capturable() const override { return true; }
   void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
-                 const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s);
-  void allreduce_max_f32(float* buf, size_t n, hipStream_t s);
-  void allreduce_sum_f64(double* buf, size_t n, hipStream_t s);
-  void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s);
-  void broadcast(void* buf, size_t bytes, int root, hipStream_t s);
-  void abort();
+                 const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
+  void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
+  void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
+  void abort() override;
 
  private:
-  int rank_ = 0, size_ = 1;
   void* comm_ = nullptr;  // ncclComm_t
+};
+
+class ShmComm final : public Comm {
+ public:
+  ShmComm(int rank, int nranks, const std::string& name);
+  ~ShmComm() override;
+  bool graph_capturable() const override { return false; }
+  void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
+                 const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
+  void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
+  void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
+  void abort() override {}
+
+ private:
+  void barrier();
+  char* slot(int src, int dst);
+  template <typename T, typename Op>
+  void allreduce(T* buf, size_t n, hipStream_t s, Op op);
+  std::string name_;
+  void* base_ = nullptr;
+  size_t bytes_ = 0, slot_bytes_ = 0;
 };
 
 }  // namespace channel

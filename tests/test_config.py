@@ -1,0 +1,80 @@
+"""run.conf parser (C++), mirroring the reference's libconfig keys (run.conf:1-23, config.c:4-42)."""
+import os
+
+import pytest
+
+REF_STYLE = """
+application:
+{
+	NX = 128;
+	NY = 128;
+	NZ = 65; #Points in physical space are 2*NZ+2
+	input:
+	{
+ 		G = "-";
+		DDV = "-";
+		UMEAN = "-";
+		# G = "/drive1/x/G.h5";
+	};
+	output:
+	{
+		G = "/tmp/G.01.h5";
+		DDV = "/tmp/ddV.01.h5";
+		UMEAN = "/tmp/Umean2.bin";
+	};
+	path = "/tmp/out/";
+};
+"""
+
+
+def test_reference_keys(native):
+    c = native.Config.from_string(REF_STYLE)
+    assert (c.NX, c.NY, c.NZ) == (128, 128, 65)
+    assert c.nzp == 128
+    assert c.in_G == "-" and c.in_DDV == "-" and c.in_UMEAN == "-"
+    assert c.out_G == "/tmp/G.01.h5" and c.out_UMEAN == "/tmp/Umean2.bin"
+    assert c.path == "/tmp/out/"
+    # reference constants as defaults (channel.h:50-62, RK3.c:68, 124)
+    assert c.Re == 3250.0 and c.Q == 1.8 and c.cfl == 0.5 and c.nsteps == 30000 and c.stats_every == 10
+
+
+def test_overrides_and_roundtrip(native):
+    c = native.Config.from_string(REF_STYLE, ["Re=5000", "nsteps=10", 'precision="fp64"', "NY=129"])
+    assert c.Re == 5000.0 and c.nsteps == 10 and c.precision == "fp64" and c.NY == 129
+    c2 = native.Config.from_string(c.to_string())
+    for k in ["NX", "NY", "NZ", "Re", "Q", "LX", "LZ", "nsteps", "cfl", "precision", "path", "out_G", "seed", "ic"]:
+        assert getattr(c2, k) == getattr(c, k), k
+
+
+def test_comments_and_toplevel_keys(native):
+    c = native.Config.from_string("""
+        /* block comment */
+        NX = 64; // line comment
+        NY = 65;
+        NZ = 33;
+        Re = 1e3;
+        health_check = false;
+    """)
+    assert (c.NX, c.NY, c.NZ, c.Re, c.health_check) == (64, 65, 33, 1000.0, False)
+
+
+def test_file_and_example(native):
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    c = native.Config.from_file(os.path.join(here, "configs", "run.conf"))
+    assert c.NX == 128 and c.nsteps == 100 and c.out_G == "G.h5"
+
+
+@pytest.mark.parametrize("bad", ["NX = 100; NY = 33; NZ = 17;",      # NX not a power of two
+                                 "NX = 64; NY = 33; NZ = 16;",       # 2NZ-2 not a power of two
+                                 "NX = 64; NY = 3; NZ = 17;",        # NY too small
+                                 "NX = 64; NY = 33; NZ = 17; precision = \"bf16\";",
+                                 "NX = 64 NY = 33;",                 # syntax
+                                 "application: { NX = 64;"])         # unterminated group
+def test_invalid(native, bad):
+    with pytest.raises(RuntimeError):
+        native.Config.from_string(bad)
+
+
+def test_input_files_imply_file_ic(native):
+    c = native.Config.from_string('NX=32; NY=33; NZ=17; input: { G = "g.h5"; DDV = "d.h5"; };')
+    assert c.ic == "file"

@@ -1,0 +1,81 @@
+"""Slab-decomposed GPU solver with P ranks sharing the one GPU of the test box.
+
+RCCL refuses two ranks on one device, so these runs use the host shared-memory communicator
+(ShmComm, "shm:" unique id), which drives exactly the same send/recv block addressing, x-transform
+source/destination tables and reductions as the RCCL path.  The P-rank trajectory must equal the
+NumPy oracle, and a restart written by P ranks must be readable by one rank.
+"""
+import os
+import tempfile
+import uuid
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from channel_gpu_amd.reference import oracle as ora
+
+pytestmark = pytest.mark.gpu
+
+GRID = dict(NX=32, NY=33, NZ=17)
+
+
+def _global_state():
+    plan = ora.OraclePlan(**GRID)
+    ops = ora.build_ops(GRID["NY"])
+    phi, om = ora.random_state(plan, ops, seed=5, amp=0.3)
+    return phi, om, 0.75 * 1.8 * (1 - ops.y ** 2)
+
+
+def _worker(rank, world, shm, outdir, nsteps):
+    import torch  # noqa: F401
+
+    from channel_gpu_amd import require_native
+    from channel_gpu_amd.utils.config import default_config
+
+    C = require_native()
+    cfg = default_config(**GRID, Re=400.0, precision="fp64", dt_fixed=0.01, ic="zero", stats_every=0,
+                         log_every=0, symmetry_every=0)
+    s = C.Solver(cfg, rank, world, 0, shm.encode())
+    p = s.plan
+    phi, om, U = _global_state()
+    sl = slice(p.kx0, p.kx0 + p.nkx_loc)
+    s.set_state(np.ascontiguousarray(phi[:, sl]), np.ascontiguousarray(om[:, sl]), U)
+    s.prepare()
+    for _ in range(nsteps):
+        s.step(False)
+    gphi, gom, gU = s.get_state()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), phi=gphi, om=gom, U=gU, health=s.health())
+    if C.hdf5_available():
+        s.write_restart(os.path.join(outdir, "G.h5"), os.path.join(outdir, "DDV.h5"), os.path.join(outdir, "U.bin"))
+    del s
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_matches_oracle(native, world):
+    nsteps = 2
+    ref = ora.OracleSolver(**GRID, Re=400.0, dt_fixed=0.01)
+    phi, om, U = _global_state()
+    ref.set_state(phi, om, U)
+    for _ in range(nsteps):
+        ref.step()
+    shm = f"shm:chtest_{uuid.uuid4().hex[:12]}"
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, shm, d, nsteps), nprocs=world, join=True, start_method="spawn")
+        parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+        gphi = np.concatenate([q["phi"] for q in parts], axis=1)
+        gom = np.concatenate([q["om"] for q in parts], axis=1)
+        assert all(int(q["health"]) == 0 for q in parts)
+        assert np.abs(gphi - ref.phi).max() < 1e-9 * np.abs(ref.phi).max()
+        assert np.abs(gom - ref.om).max() < 1e-9 * np.abs(ref.om).max()
+        assert np.abs(parts[0]["U"] - ref.U).max() < 1e-11
+        if native.hdf5_available():
+            from channel_gpu_amd.utils.config import default_config
+
+            cfg = default_config(**GRID, Re=400.0, precision="fp64", ic="zero", stats_every=0, log_every=0)
+            s1 = native.Solver(cfg, 0, 1, 0, b"")
+            s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), os.path.join(d, "U.bin"))
+            rphi, rom, rU = s1.get_state()
+            # files hold float32 (reference format)
+            assert np.abs(rphi - ref.phi).max() < 1e-5 * np.abs(ref.phi).max()
+            assert np.abs(rU - ref.U).max() < 1e-5

@@ -1,0 +1,63 @@
+"""Slab decomposition math: C++ Plan vs the Python mirror; limits of the reference lifted
+(NX != NY, NY % P != 0, NY = 385 at P = 8)."""
+import pytest
+
+from channel_gpu_amd.parallel.decomposition import SlabDecomposition, balanced_split
+
+
+def cfg(native, **kw):
+    c = native.Config()
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_plan_matches_python(native, P):
+    c = cfg(native, NX=1024, NY=385, NZ=513)
+    d = SlabDecomposition(1024, 385, 513, P)
+    ks, kc = d.kx_split()
+    ys, yc = d.y_split()
+    for r in range(P):
+        p = native.Plan.make(c, P, r)
+        assert (p.nkx, p.nkz, p.Kx, p.Kz) == (683, 342, 341, 341)
+        assert p.kx0 == ks[r] and p.nkx_loc == kc[r]
+        assert p.y0 == ys[r] and p.ny_loc == yc[r]
+        assert p.R == 7
+    assert sum(kc) == 683 and sum(yc) == 385 and max(yc) - min(yc) <= 1
+
+
+def test_mean_mode_on_rank0(native):
+    c = cfg(native, NX=128, NY=129, NZ=65)
+    p = native.Plan.make(c, 4, 0)
+    assert p.kx0 == 0 and p.kx_of(0) == 0
+
+
+def test_kx_maps(native):
+    c = cfg(native, NX=128, NY=129, NZ=65)
+    p = native.Plan.make(c, 1, 0)
+    assert p.nkx == 85 and p.Kx == 42
+    assert p.kx_of(42) == 42 and p.kx_of(43) == -42 and p.kx_of(84) == -1
+    assert p.kx_fft_pos(43) == 128 - 42 and p.kx_fft_pos(84) == 127
+
+
+def test_balanced_split_properties():
+    for n in (33, 385, 683):
+        for parts in (1, 2, 3, 7, 8):
+            s, c = balanced_split(n, parts)
+            assert sum(c) == n and s[0] == 0 and max(c) - min(c) <= 1
+            assert all(s[i] + c[i] == s[i + 1] for i in range(parts - 1))
+
+
+def test_too_many_ranks(native):
+    c = cfg(native, NX=32, NY=33, NZ=17)
+    with pytest.raises(RuntimeError):
+        native.Plan.make(c, 64, 0)
+
+
+def test_a2a_volume_model():
+    d = SlabDecomposition(1024, 385, 1024 // 2 + 1, 8)
+    b = d.a2a_off_rank_bytes_per_step(esz=8)
+    # per rank and step: 27 transposes of 7/8 of its retained-field slab (0.72 GB / 8 per field)
+    # ~= 2.1 GB; at ~7 x 153 GB/s of xGMI per GPU that is ~2 ms of ideal all-to-all per step
+    assert 1.5e9 < b < 3.0e9
