@@ -1,0 +1,116 @@
+#include "channel/bootstrap.hpp"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "channel/common.hpp"
+
+namespace channel {
+
+namespace {
+int env_int(std::initializer_list<const char*> names, int dflt) {
+  for (const char* n : names) {
+    const char* v = std::getenv(n);
+    if (v && *v) return std::atoi(v);
+  }
+  return dflt;
+}
+
+void send_all(int fd, const void* buf, size_t n) {
+  const char* p = static_cast<const char*>(buf);
+  while (n) {
+    ssize_t k = ::send(fd, p, n, 0);
+    CH_CHECK(k > 0, "bootstrap send failed");
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+}
+
+void recv_all(int fd, void* buf, size_t n) {
+  char* p = static_cast<char*>(buf);
+  while (n) {
+    ssize_t k = ::recv(fd, p, n, 0);
+    CH_CHECK(k > 0, "bootstrap recv failed");
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+}
+}  // namespace
+
+ProcInfo ProcInfo::from_env() {
+  ProcInfo p;
+  p.rank = env_int({"RANK", "PMI_RANK", "OMPI_COMM_WORLD_RANK", "SLURM_PROCID"}, 0);
+  p.size = env_int({"WORLD_SIZE", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE", "SLURM_NTASKS"}, 1);
+  p.local_rank = env_int({"LOCAL_RANK", "MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID"}, p.rank);
+  CH_CHECK(p.size >= 1 && p.rank >= 0 && p.rank < p.size, "bad rank/size " << p.rank << "/" << p.size);
+  return p;
+}
+
+std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int timeout_s) {
+  if (pi.size == 1) return payload;
+  const char* addr_s = std::getenv("MASTER_ADDR");
+  const char* port_s = std::getenv("MASTER_PORT");
+  const std::string addr = addr_s && *addr_s ? addr_s : "127.0.0.1";
+  // use a port distinct from torchrun's store port
+  const int port = (port_s && *port_s ? std::atoi(port_s) : 29500) + 11;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
+  if (pi.rank == 0) {
+    int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+    CH_CHECK(ls >= 0, "socket failed");
+    int one = 1;
+    setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons(static_cast<uint16_t>(port));
+    sa.sin_addr.s_addr = htonl(INADDR_ANY);
+    CH_CHECK(::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0, "bind to port " << port << " failed");
+    CH_CHECK(::listen(ls, pi.size) == 0, "listen failed");
+    for (int i = 1; i < pi.size; ++i) {
+      int fd = ::accept(ls, nullptr, nullptr);
+      CH_CHECK(fd >= 0, "accept failed");
+      int32_t peer = -1;
+      recv_all(fd, &peer, sizeof(peer));
+      const uint64_t n = payload.size();
+      send_all(fd, &n, sizeof(n));
+      send_all(fd, payload.data(), payload.size());
+      ::close(fd);
+    }
+    ::close(ls);
+    return payload;
+  }
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  CH_CHECK(getaddrinfo(addr.c_str(), std::to_string(port).c_str(), &hints, &res) == 0 && res,
+           "cannot resolve MASTER_ADDR " << addr);
+  int fd = -1;
+  while (true) {
+    fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) break;
+    ::close(fd);
+    CH_CHECK(std::chrono::steady_clock::now() < deadline, "bootstrap connect timeout to " << addr << ":" << port);
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+  freeaddrinfo(res);
+  const int32_t me = pi.rank;
+  send_all(fd, &me, sizeof(me));
+  uint64_t n = 0;
+  recv_all(fd, &n, sizeof(n));
+  std::string out(n, '\0');
+  recv_all(fd, out.data(), n);
+  ::close(fd);
+  return out;
+}
+
+}  // namespace channel

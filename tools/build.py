@@ -106,14 +106,12 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
         _run([HIPCC, "-shared", "-fPIC", bobj, "-o", EXT_SO, f"-L{LIBDIR}", "-lchannel_core", *tld,
               "-Wl,-rpath,$ORIGIN/lib"], verbose)
     if driver:
+        # the driver bootstraps RCCL over TCP (csrc/core/bootstrap.cpp): no MPI link dependency
         dsrc = os.path.join(ROOT, "csrc", "driver", "main.cpp")
-        if os.path.exists(dsrc) and os.path.exists(os.path.join(CONDA, "include", "mpi.h")):
-            os.makedirs(os.path.dirname(DRIVER), exist_ok=True)
-            if _stale(DRIVER, [dsrc, CORE_SO], hdr):
-                _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", f"-I{CONDA}/include", dsrc, "-o", DRIVER,
-                      f"-L{LIBDIR}", "-lchannel_core", f"-L{CONDA}/lib", "-lmpi",
-                      "-Wl,-rpath,$ORIGIN/../channel_gpu_amd/lib", "-Wl,-rpath,/opt/rocm/lib",
-                      f"-Wl,-rpath,{CONDA}/lib"], verbose)
+        os.makedirs(os.path.dirname(DRIVER), exist_ok=True)
+        if _stale(DRIVER, [dsrc, CORE_SO], hdr):
+            _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", dsrc, "-o", DRIVER, f"-L{LIBDIR}", "-lchannel_core",
+                  "-Wl,-rpath,$ORIGIN/../channel_gpu_amd/lib", "-Wl,-rpath,/opt/rocm/lib"], verbose)
 
 
 def main() -> None:
