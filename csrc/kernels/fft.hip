@@ -50,10 +50,14 @@ void Twiddles::release() {
 }
 
 // ---- x-direction -------------------------------------------------------------------------
+constexpr int xcfg_c(int nx, int tsz) { return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 1024 ? 4 : 8); }
+constexpr int xcfg_nt(int nx, int tsz) { return 256 + 0 * nx * tsz; }
+
 template <int NX, typename T>
 struct XCfg {
-  static constexpr int C = sizeof(T) == 4 ? (NX >= 1024 ? 8 : 16) : (NX >= 1024 ? 4 : 8);
-  static constexpr int NT = 256;
+  // kz columns per tile (64-B segments; 128-B tiles measured slower: 1 block/CU)
+  static constexpr int C = xcfg_c(NX, sizeof(T));
+  static constexpr int NT = xcfg_nt(NX, sizeof(T));
   // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
   // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
   static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
@@ -67,12 +71,14 @@ __device__ __forceinline__ int find_block(const int* start, int n, int i) {
 }
 
 template <int NX, typename T>
-__global__ void __launch_bounds__(256) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
+__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T))) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
                                                             const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   __shared__ T2 s[C * PITCH];
+  __shared__ T2 tws[NX];  // twiddles staged per block (LDS latency in the dependent passes)
+  for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const unsigned t = xcd_remap(blockIdx.x, gridDim.x);  // adjacent kz chunks of one (y, f) share an XCD
   const int kz0 = static_cast<int>(t % nkzc) * C;
@@ -107,7 +113,7 @@ __global__ void __launch_bounds__(256) xfft_backward_kernel(XArgs a, XSrc src, t
   __syncthreads();
   {
     constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
-    wave_fft<NX, RW, PITCH, true>(s + (tid / 64) * RW * PITCH, tw, tid & 63);
+    wave_fft<NX, RW, PITCH, true>(s + (tid / 64) * RW * PITCH, tws, tid & 63);
   }
   __syncthreads();
   T2* out = phys + f * a.field_stride_phys;
@@ -119,12 +125,14 @@ __global__ void __launch_bounds__(256) xfft_backward_kernel(XArgs a, XSrc src, t
 }
 
 template <int NX, typename T>
-__global__ void __launch_bounds__(256) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
+__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T))) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
                                                            const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   __shared__ T2 s[C * PITCH];
+  __shared__ T2 tws[NX];  // twiddles staged per block (LDS latency in the dependent passes)
+  for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
   const int kz0 = static_cast<int>(t % nkzc) * C;
@@ -151,7 +159,7 @@ __global__ void __launch_bounds__(256) xfft_forward_kernel(XArgs a, const typena
   __syncthreads();
   {
     constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
-    wave_fft<NX, RW, PITCH, false>(s + (tid / 64) * RW * PITCH, tw, tid & 63);
+    wave_fft<NX, RW, PITCH, false>(s + (tid / 64) * RW * PITCH, tws, tid & 63);
   }
   __syncthreads();
   T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
@@ -184,10 +192,14 @@ template <typename T>
 static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
-    constexpr int C = XCfg<NN, T>::C;
-    dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
-    hipLaunchKernelGGL((xfft_backward_kernel<NN, T>), grid, dim3(256), 0, s, a, src, static_cast<T2*>(phys),
-                       static_cast<const T2*>(tw.buf));
+    if constexpr (sizeof(T) == 8 && NN > 1024) {
+      CH_CHECK(false, "fp64 storage supports NX <= 1024");
+    } else {
+      constexpr int C = XCfg<NN, T>::C;
+      dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
+      hipLaunchKernelGGL((xfft_backward_kernel<NN, T>), grid, dim3(XCfg<NN, T>::NT), 0, s, a, src, static_cast<T2*>(phys),
+                         static_cast<const T2*>(tw.buf));
+    }
   });
   HIP_LAUNCH_CHECK(s);
 }
@@ -196,10 +208,14 @@ template <typename T>
 static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
-    constexpr int C = XCfg<NN, T>::C;
-    dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
-    hipLaunchKernelGGL((xfft_forward_kernel<NN, T>), grid, dim3(256), 0, s, a, static_cast<const T2*>(phys), dst,
-                       static_cast<const T2*>(tw.buf));
+    if constexpr (sizeof(T) == 8 && NN > 1024) {
+      CH_CHECK(false, "fp64 storage supports NX <= 1024");
+    } else {
+      constexpr int C = XCfg<NN, T>::C;
+      dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
+      hipLaunchKernelGGL((xfft_forward_kernel<NN, T>), grid, dim3(XCfg<NN, T>::NT), 0, s, a, static_cast<const T2*>(phys), dst,
+                         static_cast<const T2*>(tw.buf));
+    }
   });
   HIP_LAUNCH_CHECK(s);
 }
@@ -234,8 +250,11 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   constexpr int PITCH = FftPitch<NZP>::value;
   constexpr int EP = (NZP + 63) / 64;  // points per lane
   __shared__ T2 s[ZW * PITCH];
+  __shared__ T2 tws[NZP];  // twiddles staged once per block: LDS latency instead of L2 in the passes
   __shared__ float red[4][ZW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < NZP; i += ZW * 64) tws[i] = tw[i];
+  __syncthreads();
   T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   const long long r = static_cast<long long>(blockIdx.x) * ZW + w;
@@ -273,7 +292,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
       }
       for (int k = Kz + 1 + lane; k < NZP - Kz; k += 64) row[fft_pidx(k)] = T2{0, 0};
       __builtin_amdgcn_wave_barrier();
-      wave_fft<NZP, 1, PITCH, true>(row, tw, lane);
+      wave_fft<NZP, 1, PITCH, true>(row, tws, lane);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
         const int n = lane + 64 * i;
@@ -300,7 +319,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     }
     __builtin_amdgcn_wave_barrier();
     const T sc = static_cast<T>(0.5 * a.scale);
-    wave_fft<NZP, 1, PITCH, false>(row, tw, lane);
+    wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     for (int k = lane; k < nkz; k += 64) {
       const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
@@ -314,7 +333,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
       if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
     }
     __builtin_amdgcn_wave_barrier();
-    wave_fft<NZP, 1, PITCH, false>(row, tw, lane);
+    wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
     for (int k = lane; k < nkz; k += 64) {
       const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
       fields[2 * fs + r * nkz + k] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
