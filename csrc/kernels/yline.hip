@@ -15,6 +15,7 @@
 // matrix multiplies the equation), so the explicit viscous term needs no solve at all.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -287,17 +288,23 @@ struct SpecTile {
   static constexpr int PLANE = 64 * PITCH + 1;
   T2* tile;
   int N, lines, line0, w, lane;
+  T2 pend[R];  // this thread's share of the next field, in flight while the current one is used
 
-  __device__ void load(const T2* __restrict__ src, double (&x)[2][R]) const {
-    // all global loads of a thread in flight together (N*W <= 64*R*W => at most R per thread)
-    T2 v[R];
+  // Issue the global loads of a field (N*W <= 64*R*W => at most R per thread) without waiting:
+  // the kernel prefetches field k+1 before computing on field k, so at one wave per SIMD the HBM
+  // latency of each staging overlaps the fp64 line solves instead of stalling the whole block.
+  __device__ void prefetch(const T2* __restrict__ src) { prefetch_at(src, line0); }
+  __device__ void prefetch_at(const T2* __restrict__ src, int l0) {
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int e = threadIdx.x + q * W * 64;
       const int y = e / W, l = e - y * W;
-      v[q] = T2{0, 0};
-      if (e < N * W && line0 + l < lines) v[q] = src[static_cast<size_t>(y) * lines + line0 + l];
+      pend[q] = T2{0, 0};
+      if (e < N * W && l0 + l < lines) pend[q] = src[static_cast<size_t>(y) * lines + l0 + l];
     }
+  }
+  // Stage the prefetched field through the LDS tile and return this wave's line.
+  __device__ void commit(double (&x)[2][R]) const {
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -305,10 +312,16 @@ struct SpecTile {
       if (e < N * W) {
         const int y = e / W, l = e - y * W;
         const int ly = y / R, r = y - ly * R;
-        tile[r * PLANE + ly * PITCH + l] = v[q];
+        tile[r * PLANE + ly * PITCH + l] = pend[q];
       }
     }
     __syncthreads();
+    column(x);
+  }
+  // This wave's line as it sits in the tile.  After store() the tile still holds the stored
+  // field, so a value just written out can be re-read from LDS (at storage precision) without
+  // a global round trip, as long as no staging has happened since.
+  __device__ void column(double (&x)[2][R]) const {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = lane * R + r;
@@ -316,6 +329,10 @@ struct SpecTile {
       x[0][r] = j < N ? static_cast<double>(v.x) : 0.0;
       x[1][r] = j < N ? static_cast<double>(v.y) : 0.0;
     }
+  }
+  __device__ void load(const T2* __restrict__ src, double (&x)[2][R]) {
+    prefetch(src);
+    commit(x);
   }
   __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) const {
     __syncthreads();
@@ -376,12 +393,22 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   static_assert(sizeof(T2) * (W + 1) >= 4 * sizeof(double), "tile too small for the stats reduction");
   const int lane = __lane_id();
   const int w = threadIdx.x / 64;
-  // XCD-aware tile order: tiles adjacent in memory (partial 128-B lines) land in one L2
-  const int line0 = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x)) * W;
+  const int N = a.N;
+  // Persistent blocks: the grid is sized to the resident capacity (one block per CU at the R=7
+  // register budget) and each block walks tiles of W lines, so the coefficient tables are staged
+  // into LDS once per block instead of once per tile, and the first field of the next tile is
+  // prefetched while the current tile's outputs drain.  XCD-aware order: at each iteration the
+  // blocks of one XCD take consecutive tiles, which share partial 128-B lines in that L2.
+  const int ntiles = (a.lines + W - 1) / W;
+  const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  SpecTile<R, T, W> st{tile_mem, N, a.lines, lb * W, w, lane};
+  if (a.mode == 1 && lb < ntiles) st.prefetch(static_cast<const T2*>(a.out[0]));  // H_x of the first tile
+  for (int tile = lb; tile < ntiles; tile += gridDim.x) {
+  const int line0 = tile * W;
+  st.line0 = line0;
   const int line = line0 + w;
   const bool valid = line < a.lines;
-  const int N = a.N;
-  SpecTile<R, T, W> st{tile_mem, N, a.lines, line0, w, lane};
+  const int next_line0 = (tile + static_cast<int>(gridDim.x)) * W;
 
   const int ikx = valid ? line / a.nkz : 0;
   const int kz = valid ? line - ikx * a.nkz : 0;
@@ -410,11 +437,15 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     const double dt = *a.dt;
     double RPn[2][R], RWn[2][R];
     // ---------------- nonlinear terms h_v, h_g in M-form -----------------------------------
+    // Staging is software-pipelined: each field's global loads are issued (prefetch) before the
+    // arithmetic on the previous field, and only committed through LDS when needed.  H_x of this
+    // tile was prefetched by the previous iteration (or before the loop).
     {
       double X[2][R], G[2][R];
       {
         double H[2][R];
-        st.load(out[0], H);  // H_x
+        st.commit(H);
+        st.prefetch(out[2]);  // H_z
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           X[0][r] = al * H[1][r];   // -i al Hx
@@ -422,7 +453,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           G[0][r] = is_mean ? H[0][r] : -be * H[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
           G[1][r] = is_mean ? 0.0 : be * H[0][r];
         }
-        st.load(out[2], H);  // H_z
+        st.commit(H);
+        st.prefetch(out[1]);  // H_y
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           X[0][r] += be * H[1][r];  // -i be Hz
@@ -434,7 +466,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       d1_apply<R, 2>(t, X, lane);  // D(-i al Hx - i be Hz)
       {
         double Hy[2][R];
-        st.load(out[1], Hy);
+        st.commit(Hy);
+        st.prefetch(phi);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -455,7 +488,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     double rhsP[2][R], rhsW[2][R];
     {
       double q[2][R], Mq[2][R], Kq[2][R];
-      st.load(phi, q);
+      const bool zprev = a.rk_z != 0.0;
+      st.commit(q);
+      st.prefetch(omega);
       apply_M<R, 2>(t, q, Mq, lane);
       apply_K<R, 2>(t, q, Kq, lane);
 #pragma unroll
@@ -463,7 +498,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
           rhsP[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RPn[k][r]);
-      st.load(omega, q);
+      st.commit(q);
+      if (zprev) st.prefetch(Rphi);
       apply_M<R, 2>(t, q, Mq, lane);
       apply_K<R, 2>(t, q, Kq, lane);
 #pragma unroll
@@ -471,13 +507,14 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
           rhsW[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RWn[k][r]);
-      if (a.rk_z != 0.0) {
-        st.load(Rphi, q);
+      if (zprev) {
+        st.commit(q);
+        st.prefetch(Romega);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
           for (int r = 0; r < R; ++r) rhsP[k][r] += dt * a.rk_z * q[k][r];
-        st.load(Romega, q);
+        st.commit(q);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -586,8 +623,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         czero<R>(v);
       }
     }
+    // omega was the last field staged (store above): re-read it from the tile, not from HBM
+    st.column(om);
     st.store(phi, ph);
-    st.load(omega, om);  // reload (cheaper than keeping 2R doubles live through the influence step)
   } else {
     // ---------------- prepare only: fields from the state ----------------------------------
     st.load(phi, ph);
@@ -665,6 +703,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
     }
   }
+  if (a.mode == 1 && next_line0 < a.lines) st.prefetch_at(out[0], next_line0);  // next tile's H_x
   st.store(out[0], fu);
   st.store(out[1], v);
   st.store(out[2], fw);
@@ -717,6 +756,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       a.mean_diag[3 * N + 3] = mean_C;
     }
   }
+  }  // tile loop
 }
 
 template <int R, typename T>
@@ -727,8 +767,19 @@ constexpr int kspec_waves() {
 template <int R, typename T>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_waves<R, T>();
-  dim3 grid((a.lines + W - 1) / W), block(W * 64);
-  hipLaunchKernelGGL((kspec_kernel<R, T, W>), grid, block, 0, stream, t.tab, a);
+  auto kern = kspec_kernel<R, T, W>;
+  // persistent grid: as many blocks as can be resident at once (queried once per instantiation)
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, W * 64, 0));
+    resident = std::max(1, cus) * std::max(1, per_cu);
+  }
+  const int ntiles = (a.lines + W - 1) / W;
+  dim3 grid(std::min(ntiles, resident)), block(W * 64);
+  hipLaunchKernelGGL(kern, grid, block, 0, stream, t.tab, a);
 }
 
 void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream) {
