@@ -8,6 +8,7 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <mutex>
 
 #include "channel/common.hpp"
 #include "channel/io.hpp"
@@ -55,6 +56,22 @@ void thomas(const std::vector<double>& a, const std::vector<double>& b, const st
 
 bool debug_sync_enabled() { return g_debug_sync; }
 void set_debug_sync(bool on) { g_debug_sync = on; }
+
+int resident_blocks(const void* kernel, int threads, size_t dyn_lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int> cache;
+  int dev = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({dev, kernel});
+  if (it != cache.end()) return it->second;
+  int cus = 0, per_cu = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, dyn_lds));
+  const int n = std::max(1, cus) * std::max(1, per_cu);
+  cache[{dev, kernel}] = n;
+  return n;
+}
 
 Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::string& nccl_uid)
     : cfg_(cfg), plan_(Plan::make(cfg, nranks, rank)), grid_(YGrid::build(cfg.NY, cfg.stretch)), device_(device) {

@@ -30,6 +30,11 @@ struct Error : std::runtime_error {
 bool debug_sync_enabled();
 void set_debug_sync(bool on);
 
+// Number of blocks of `kernel` (with `threads` per block and `dyn_lds` dynamic LDS) that are
+// resident on the current device at once: CUs x occupancy.  Persistent kernels size their grid
+// with it.  Cached per (device, kernel).
+int resident_blocks(const void* kernel, int threads, size_t dyn_lds = 0);
+
 }  // namespace channel
 
 #define CH_CHECK(cond, msg)                                          \

@@ -14,6 +14,7 @@
 //    the per-destination all-to-all send blocks (or, for P=1, into the spectral H arrays).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -70,107 +71,142 @@ __device__ __forceinline__ int find_block(const int* start, int n, int i) {
   return s;
 }
 
+// Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
+// LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
+// into registers right after the current tile is staged into LDS, so they are in flight during
+// the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
+// block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
 template <int NX, typename T>
-__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T))) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
+__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
                                                             const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
+  constexpr int NKMAX = 2 * (NX / 3) + 1;
+  constexpr int EPT = (NKMAX * C + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
-  __shared__ T2 tws[NX];  // twiddles staged per block (LDS latency in the dependent passes)
+  __shared__ T2 tws[NX];
   for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
-  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);  // adjacent kz chunks of one (y, f) share an XCD
-  const int kz0 = static_cast<int>(t % nkzc) * C;
-  const int rest = static_cast<int>(t / nkzc);
-  const int y = rest % a.ny, f = rest / a.ny;
+  const int ntiles = a.ny * nkzc * a.nfields;
+  const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
-  const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
-  // issue every global load of this thread before touching LDS (one latency, not EPT of them)
-  constexpr int EPT = (NX * C + NT - 1) / NT;
+  const int nload = a.nkx * C;
   T2 v[EPT];
+  // tile t -> (f, y, kz0); at each iteration the blocks of one XCD take consecutive tiles
+  auto fetch = [&](int t) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * NT;
-    const int x = e / C, c = e - x * C;
-    const int kz = kz0 + c;
-    int i = -1;
-    if (x <= a.Kx) i = x;
-    else if (x >= NX - a.Kx) i = a.nkx - (NX - x);
-    v[q] = T2{0, 0};
-    if (e < NX * C && i >= 0 && kz < a.nkz) {
-      const int sb = find_block(src.kx_start, src.nsrc, i);
-      const int nk = src.kx_start[sb + 1] - src.kx_start[sb];
-      v[q] = base[src.off[sb] + (static_cast<long long>(y) * nk + (i - src.kx_start[sb])) * a.nkz + kz];
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int i = e / C, c = e - i * C;
+      const int kz = kz0 + c;
+      v[q] = T2{0, 0};
+      if (e < nload && kz < a.nkz) {
+        const int sb = find_block(src.kx_start, src.nsrc, i);
+        const int nk = src.kx_start[sb + 1] - src.kx_start[sb];
+        // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
+        v[q] = base[static_cast<unsigned>(src.off[sb] + (static_cast<long long>(y) * nk + (i - src.kx_start[sb])) * a.nkz + kz)];
+      }
     }
-  }
+  };
+  int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  if (t < ntiles) fetch(t);
+  for (; t < ntiles; t += G) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    __syncthreads();  // previous tile's stores have finished reading s
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * NT;
-    const int x = e / C, c = e - x * C;
-    if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
-  }
-  __syncthreads();
-  {
-    constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
-    wave_fft<NX, RW, PITCH, true>(s + (tid / 64) * RW * PITCH, tws, tid & 63);
-  }
-  __syncthreads();
-  T2* out = phys + f * a.field_stride_phys;
-  for (int e = tid; e < NX * C; e += NT) {
-    const int x = e / C, c = e - x * C;
-    const int kz = kz0 + c;
-    if (kz < a.nkz) out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int i = e / C, c = e - i * C;
+      const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+      if (e < nload) s[c * PITCH + fft_pidx(x)] = v[q];
+    }
+    for (int e = tid; e < (NX - a.nkx) * C; e += NT) {
+      const int j = e / C, c = e - j * C;
+      s[c * PITCH + fft_pidx(a.Kx + 1 + j)] = T2{0, 0};
+    }
+    __syncthreads();
+    if (t + G < ntiles) fetch(t + G);
+    {
+      constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
+      // one row at a time: the prefetched next tile already holds EPT registers
+#pragma unroll 1
+      for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, true>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+    }
+    __syncthreads();
+    T2* out = phys + f * a.field_stride_phys;
+    for (int e = tid; e < NX * C; e += NT) {
+      const int x = e / C, c = e - x * C;
+      const int kz = kz0 + c;
+      if (kz < a.nkz) out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+    }
   }
 }
 
 template <int NX, typename T>
-__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T))) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
+__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
                                                            const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  constexpr int EPT = (NX * C + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
-  __shared__ T2 tws[NX];  // twiddles staged per block (LDS latency in the dependent passes)
+  __shared__ T2 tws[NX];
   for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
-  const unsigned t = xcd_remap(blockIdx.x, gridDim.x);
-  const int kz0 = static_cast<int>(t % nkzc) * C;
-  const int rest = static_cast<int>(t / nkzc);
-  const int y = rest % a.ny, f = rest / a.ny;
+  const int ntiles = a.ny * nkzc * a.nfields;
+  const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
-  const T2* in = phys + f * a.field_stride_phys;
-  constexpr int EPT = (NX * C + NT - 1) / NT;
   T2 v[EPT];
+  auto fetch = [&](int t) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    const T2* in = phys + f * a.field_stride_phys;
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * NT;
-    const int x = e / C, c = e - x * C;
-    const int kz = kz0 + c;
-    v[q] = T2{0, 0};
-    if (e < NX * C && kz < a.nkz) v[q] = in[(static_cast<long long>(y) * NX + x) * a.nkz + kz];
-  }
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int x = e / C, c = e - x * C;
+      const int kz = kz0 + c;
+      v[q] = T2{0, 0};
+      if (e < NX * C && kz < a.nkz) v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+    }
+  };
+  int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  if (t < ntiles) fetch(t);
+  for (; t < ntiles; t += G) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    __syncthreads();
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + q * NT;
-    const int x = e / C, c = e - x * C;
-    if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
-  }
-  __syncthreads();
-  {
-    constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
-    wave_fft<NX, RW, PITCH, false>(s + (tid / 64) * RW * PITCH, tws, tid & 63);
-  }
-  __syncthreads();
-  T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
-  for (int e = tid; e < a.nkx * C; e += NT) {
-    const int i = e / C, c = e - i * C;
-    const int kz = kz0 + c;
-    if (kz < a.nkz) {
-      const int x = i <= a.Kx ? i : NX - (a.nkx - i);
-      const int d = find_block(dst.kx_start, dst.ndst, i);
-      const int nk = dst.kx_start[d + 1] - dst.kx_start[d];
-      outb[dst.off[d] + (static_cast<long long>(y) * nk + (i - dst.kx_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int x = e / C, c = e - x * C;
+      if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
+    }
+    __syncthreads();
+    if (t + G < ntiles) fetch(t + G);
+    {
+      constexpr int RW = C / (NT / 64);
+      // one row at a time: the prefetched next tile already holds EPT registers
+#pragma unroll 1
+      for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, false>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+    }
+    __syncthreads();
+    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    for (int e = tid; e < a.nkx * C; e += NT) {
+      const int i = e / C, c = e - i * C;
+      const int kz = kz0 + c;
+      if (kz < a.nkz) {
+        const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+        const int d = find_block(dst.kx_start, dst.ndst, i);
+        const int nk = dst.kx_start[d + 1] - dst.kx_start[d];
+        outb[dst.off[d] + (static_cast<long long>(y) * nk + (i - dst.kx_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+      }
     }
   }
 }
@@ -196,8 +232,10 @@ static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddle
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
     } else {
       constexpr int C = XCfg<NN, T>::C;
-      dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
-      hipLaunchKernelGGL((xfft_backward_kernel<NN, T>), grid, dim3(XCfg<NN, T>::NT), 0, s, a, src, static_cast<T2*>(phys),
+      auto kern = xfft_backward_kernel<NN, T>;
+      const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
+      dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
+      hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, src, static_cast<T2*>(phys),
                          static_cast<const T2*>(tw.buf));
     }
   });
@@ -212,8 +250,10 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
     } else {
       constexpr int C = XCfg<NN, T>::C;
-      dim3 grid(static_cast<unsigned>(a.ny) * ((a.nkz + C - 1) / C) * a.nfields);
-      hipLaunchKernelGGL((xfft_forward_kernel<NN, T>), grid, dim3(XCfg<NN, T>::NT), 0, s, a, static_cast<const T2*>(phys), dst,
+      auto kern = xfft_forward_kernel<NN, T>;
+      const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
+      dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
+      hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                          static_cast<const T2*>(tw.buf));
     }
   });
@@ -223,12 +263,15 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s) {
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_backward: twiddle table mismatch");
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
+  CH_CHECK(a.nkx <= 2 * (a.NX / 3) + 1, "xfft_backward: more retained kx than the 2/3 rule allows");
+  CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
   if (fp64) xb_launch<double>(a, src, phys, tw, s);
   else xb_launch<float>(a, src, phys, tw, s);
 }
 
 void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s) {
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_forward: twiddle table mismatch");
+  CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_forward: per-field plane block exceeds 32-bit offsets");
   if (fp64) xf_launch<double>(a, phys, dst, tw, s);
   else xf_launch<float>(a, phys, dst, tw, s);
 }

@@ -768,17 +768,9 @@ template <int R, typename T>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_waves<R, T>();
   auto kern = kspec_kernel<R, T, W>;
-  // persistent grid: as many blocks as can be resident at once (queried once per instantiation)
-  static int resident = 0;
-  if (resident == 0) {
-    int dev = 0, cus = 0, per_cu = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, W * 64, 0));
-    resident = std::max(1, cus) * std::max(1, per_cu);
-  }
+  // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;
-  dim3 grid(std::min(ntiles, resident)), block(W * 64);
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), W * 64))), block(W * 64);
   hipLaunchKernelGGL(kern, grid, block, 0, stream, t.tab, a);
 }
 
