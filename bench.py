@@ -115,6 +115,11 @@ def main() -> None:
     }
     if args.phases:
         out["phase_ms_per_step"] = [x / max(1, args.steps) for x in solver.phase_times_ms()]
+    if os.environ.get("CHANNEL_KSPEC_PROF"):
+        # shader-clock cycles per K-SPEC phase, summed over all waves (warmup + timed steps)
+        cyc = solver.kspec_profile()
+        tot = sum(cyc) or 1.0
+        out["kspec_phase_fraction"] = [round(c / tot, 4) for c in cyc]
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

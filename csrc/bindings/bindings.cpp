@@ -323,6 +323,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_use_graph", &Solver::set_use_graph)
       .def("set_phase_timing", &Solver::set_phase_timing)
       .def("phase_times_ms", &Solver::phase_times_ms)
+      .def("kspec_profile", &Solver::kspec_profile)
       .def("symmetrize", &Solver::symmetrize)
       .def("substep_debug", &Solver::substep_debug, py::call_guard<py::gil_scoped_release>())
       .def("transforms_debug", &Solver::transforms_debug, py::call_guard<py::gil_scoped_release>())

@@ -124,8 +124,9 @@ void Solver::alloc() {
   const int N = p.NY;
   // scalars: dt, time, dtlog[8], stats[4N], mean[3N+8], invdy[N], maxima[4] (float), health
   const size_t nd = 2 + 8 + 4 * N + (3 * N + 8) + N;
-  HIP_CHECK(hipMalloc(&dscal_, nd * sizeof(double) + 4 * sizeof(float) + 16));
-  HIP_CHECK(hipMemset(dscal_, 0, nd * sizeof(double) + 4 * sizeof(float) + 16));
+  const size_t nbytes = nd * sizeof(double) + 32 + kKspecPhases * sizeof(unsigned long long);
+  HIP_CHECK(hipMalloc(&dscal_, nbytes));
+  HIP_CHECK(hipMemset(dscal_, 0, nbytes));
   double* d = static_cast<double*>(dscal_);
   d_dt_ = d;
   d_time_ = d + 1;
@@ -135,6 +136,8 @@ void Solver::alloc() {
   d_invdy_ = d_mean_ + 3 * N + 8;
   d_max_ = reinterpret_cast<float*>(d_invdy_ + N);
   d_health_ = reinterpret_cast<unsigned*>(d_max_ + 4);
+  d_kprof_ = reinterpret_cast<unsigned long long*>(static_cast<char*>(dscal_) + nd * sizeof(double) + 32);
+  kprof_on_ = std::getenv("CHANNEL_KSPEC_PROF") != nullptr;
   std::vector<double> invdy(N);
   const auto& y = grid_.y;
   for (int j = 0; j < N; ++j) {
@@ -331,6 +334,7 @@ void Solver::kspec(int mode, int n, bool stats) {
   a.stats = stats ? d_stats_ : nullptr;
   a.mean_diag = p.owns_mean() ? d_mean_ : nullptr;
   a.health = cfg_.health_check ? d_health_ : nullptr;
+  a.prof = kprof_on_ ? d_kprof_ : nullptr;
   if (stats) HIP_CHECK(hipMemsetAsync(d_stats_, 0, 4 * p.NY * sizeof(double), s_comp_));
   ev(0, false);
   kspec_launch(ytab_, a, fp64_, s_comp_);
@@ -386,6 +390,13 @@ void Solver::ev(int phase, bool end) {
 }
 
 std::vector<double> Solver::phase_times_ms() { return ph_ms_; }
+
+std::vector<double> Solver::kspec_profile() {
+  std::vector<unsigned long long> h(kKspecPhases, 0);
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  HIP_CHECK(hipMemcpy(h.data(), d_kprof_, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return std::vector<double>(h.begin(), h.end());
+}
 
 void Solver::transforms(int n, bool /*stats*/) {
   const Plan& p = plan_;

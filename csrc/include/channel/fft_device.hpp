@@ -264,6 +264,15 @@ __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restr
   if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw, lane);
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for vmcnt(0), i.e. for
+// every outstanding global load AND store of the wave (CDNA counts both on vmcnt), which
+// serialises a staging pipeline: each field's stores would have to be acknowledged by HBM before
+// the next field could be staged, and prefetched loads would be drained early.  Here only this
+// wave's LDS operations are waited for (lgkmcnt(0)) before s_barrier; the "memory" clobber keeps
+// the compiler from moving memory accesses across it.  Valid wherever the barrier only orders
+// LDS writes/reads between waves (global data exchanged between waves needs __syncthreads()).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so logical tiles that are adjacent in memory are given to blocks
 // on the same XCD (their partial cache lines then merge in one L2).  Bijective for any n.

@@ -61,7 +61,9 @@ struct SpecArgs {
   double* stats = nullptr;   // [4][N] plane sums (uu, vv, ww, uv) when non-null
   double* mean_diag = nullptr;  // [3N + 8]: U, Nx, dU/dy(walls), flux, pressure gradient ...
   unsigned* health = nullptr;   // bit 0: non-finite state
+  unsigned long long* prof = nullptr;  // [kKspecPhases] shader-clock sums per phase (debug, CHANNEL_KSPEC_PROF)
 };
+constexpr int kKspecPhases = 10;
 void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream);
 
 // ---- FFT stages ---------------------------------------------------------------------------

@@ -78,6 +78,8 @@ class Solver {
   void set_use_graph(bool on) { use_graph_ = on; }
   void set_phase_timing(bool on) { phase_timing_ = on; }
   std::vector<double> phase_times_ms();  // accumulated per-phase times (phase_timing mode)
+  // K-SPEC per-phase shader-clock sums over all waves (only with CHANNEL_KSPEC_PROF set)
+  std::vector<double> kspec_profile();
   void symmetrize();                  // kz=0 Hermitian symmetry (P == 1 only)
 
   // ---- restart files (reference-compatible, Appendix B) --------------------------------
@@ -132,6 +134,8 @@ class Solver {
   double* d_stats_ = nullptr;
   double* d_mean_ = nullptr;
   unsigned* d_health_ = nullptr;
+  unsigned long long* d_kprof_ = nullptr;
+  bool kprof_on_ = false;
   double* d_invdy_ = nullptr;
 
   std::vector<hipEvent_t> ev_a2a_, ev_xf_;

@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
   for (; t < ntiles; t += G) {
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
     const int y = rest % a.ny, f = rest / a.ny;
-    __syncthreads();  // previous tile's stores have finished reading s
+    lds_barrier();  // previous tile's stores have finished reading s
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
       const int j = e / C, c = e - j * C;
       s[c * PITCH + fft_pidx(a.Kx + 1 + j)] = T2{0, 0};
     }
-    __syncthreads();
+    lds_barrier();
     if (t + G < ntiles) fetch(t + G);
     {
       constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
 #pragma unroll 1
       for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, true>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
     }
-    __syncthreads();
+    lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
     for (int e = tid; e < NX * C; e += NT) {
       const int x = e / C, c = e - x * C;
@@ -181,14 +181,14 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
   for (; t < ntiles; t += G) {
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
     const int y = rest % a.ny, f = rest / a.ny;
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
       const int x = e / C, c = e - x * C;
       if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
     }
-    __syncthreads();
+    lds_barrier();
     if (t + G < ntiles) fetch(t + G);
     {
       constexpr int RW = C / (NT / 64);
@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
 #pragma unroll 1
       for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, false>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
     }
-    __syncthreads();
+    lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
     for (int e = tid; e < a.nkx * C; e += NT) {
       const int i = e / C, c = e - i * C;

@@ -280,7 +280,7 @@ void yline_test(const YTablesDev& t, int op, const void* in, void* out, int line
 // K-SPEC: W lines per workgroup (one wave per line); fields staged through an LDS tile
 // [r][lane][line] (pitch W+1 => conflict-free column reads), global access = W consecutive
 // complex values per y row.
-template <int R, typename T, int W>
+template <int R, typename T, int W, int NS = 1>
 struct SpecTile {
   using T2 = typename Cplx<T>::type;
   static constexpr int PITCH = W + 1;
@@ -288,34 +288,37 @@ struct SpecTile {
   static constexpr int PLANE = 64 * PITCH + 1;
   T2* tile;
   int N, lines, line0, w, lane;
-  T2 pend[R];  // this thread's share of the next field, in flight while the current one is used
+  T2 pend[NS][R];  // prefetch slots: this thread's share of fields whose loads are in flight
 
   // Issue the global loads of a field (N*W <= 64*R*W => at most R per thread) without waiting:
   // the kernel prefetches field k+1 before computing on field k, so at one wave per SIMD the HBM
   // latency of each staging overlaps the fp64 line solves instead of stalling the whole block.
-  __device__ void prefetch(const T2* __restrict__ src) { prefetch_at(src, line0); }
+  template <int S = 0>
+  __device__ void prefetch(const T2* __restrict__ src) { prefetch_at<S>(src, line0); }
+  template <int S = 0>
   __device__ void prefetch_at(const T2* __restrict__ src, int l0) {
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int e = threadIdx.x + q * W * 64;
       const int y = e / W, l = e - y * W;
-      pend[q] = T2{0, 0};
-      if (e < N * W && l0 + l < lines) pend[q] = src[static_cast<size_t>(y) * lines + l0 + l];
+      pend[S][q] = T2{0, 0};
+      if (e < N * W && l0 + l < lines) pend[S][q] = src[static_cast<size_t>(y) * lines + l0 + l];
     }
   }
   // Stage the prefetched field through the LDS tile and return this wave's line.
+  template <int S = 0>
   __device__ void commit(double (&x)[2][R]) const {
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int e = threadIdx.x + q * W * 64;
       if (e < N * W) {
         const int y = e / W, l = e - y * W;
         const int ly = y / R, r = y - ly * R;
-        tile[r * PLANE + ly * PITCH + l] = pend[q];
+        tile[r * PLANE + ly * PITCH + l] = pend[S][q];
       }
     }
-    __syncthreads();
+    lds_barrier();
     column(x);
   }
   // This wave's line as it sits in the tile.  After store() the tile still holds the stored
@@ -335,10 +338,10 @@ struct SpecTile {
     commit(x);
   }
   __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) const {
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int r = 0; r < R; ++r) tile[r * PLANE + lane * PITCH + w] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
-    __syncthreads();
+    lds_barrier();
     for (int e = threadIdx.x; e < N * W; e += W * 64) {
       const int y = e / W, l = e - y * W;
       if (line0 + l < lines) {
@@ -401,14 +404,56 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // blocks of one XCD take consecutive tiles, which share partial 128-B lines in that L2.
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
-  SpecTile<R, T, W> st{tile_mem, N, a.lines, lb * W, w, lane};
-  if (a.mode == 1 && lb < ntiles) st.prefetch(static_cast<const T2*>(a.out[0]));  // H_x of the first tile
+  SpecTile<R, T, W, 7> st{tile_mem, N, a.lines, lb * W, w, lane};
+  T2* phi = static_cast<T2*>(a.phi);
+  T2* omega = static_cast<T2*>(a.omega);
+  T2* Rphi = static_cast<T2*>(a.Rphi);
+  T2* Romega = static_cast<T2*>(a.Romega);
+  T2* out[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[i] = static_cast<T2*>(a.out[i]);
+  const bool zprev = a.rk_z != 0.0;
+  // Input staging of mode 1 is software-pipelined across tiles: the 7 input fields of the NEXT
+  // tile are loaded into register slots during the long solve phases of the current one (slots:
+  // 0 H_x, 1 H_z, 2 H_y, 3 phi, 4 omega, 5 R_phi, 6 R_omega), so at one wave per SIMD the HBM
+  // latency is hidden behind fp64 work instead of stalling each staging step.
+  auto pre_H = [&](int l0) {
+    st.template prefetch_at<0>(out[0], l0);
+    st.template prefetch_at<1>(out[2], l0);
+    st.template prefetch_at<2>(out[1], l0);
+  };
+  auto pre_S = [&](int l0) {
+    st.template prefetch_at<3>(phi, l0);
+    st.template prefetch_at<4>(omega, l0);
+  };
+  auto pre_R = [&](int l0) {
+    if (zprev) {
+      st.template prefetch_at<5>(Rphi, l0);
+      st.template prefetch_at<6>(Romega, l0);
+    }
+  };
+  if (a.mode == 1 && lb < ntiles) {
+    pre_H(lb * W);
+    pre_S(lb * W);
+    pre_R(lb * W);
+  }
+  // optional per-phase shader-clock accounting (wave-uniform, SGPRs only)
+  const bool prof_on = a.prof != nullptr;
+  unsigned long long pacc[kKspecPhases] = {};
+  unsigned long long tprev = prof_on ? __builtin_amdgcn_s_memtime() : 0;
+#define KSPEC_STAMP(k)                                           \
+  if (prof_on) {                                                 \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    pacc[k] += now_ - tprev;                                     \
+    tprev = now_;                                                \
+  }
   for (int tile = lb; tile < ntiles; tile += gridDim.x) {
   const int line0 = tile * W;
   st.line0 = line0;
   const int line = line0 + w;
   const bool valid = line < a.lines;
   const int next_line0 = (tile + static_cast<int>(gridDim.x)) * W;
+  const bool has_next = a.mode == 1 && next_line0 < a.lines;
 
   const int ikx = valid ? line / a.nkz : 0;
   const int kz = valid ? line - ikx * a.nkz : 0;
@@ -418,14 +463,6 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const double k2 = al * al + be * be;
   const bool is_mean = valid && kx == 0 && kz == 0;
   const double inv_k2 = k2 > 0.0 ? 1.0 / k2 : 0.0;
-
-  T2* phi = static_cast<T2*>(a.phi);
-  T2* omega = static_cast<T2*>(a.omega);
-  T2* Rphi = static_cast<T2*>(a.Rphi);
-  T2* Romega = static_cast<T2*>(a.Romega);
-  T2* out[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) out[i] = static_cast<T2*>(a.out[i]);
 
   double om[2][R];   // omega (state), U(y) on the mean line
   double ph[2][R];   // phi (state)
@@ -437,15 +474,11 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     const double dt = *a.dt;
     double RPn[2][R], RWn[2][R];
     // ---------------- nonlinear terms h_v, h_g in M-form -----------------------------------
-    // Staging is software-pipelined: each field's global loads are issued (prefetch) before the
-    // arithmetic on the previous field, and only committed through LDS when needed.  H_x of this
-    // tile was prefetched by the previous iteration (or before the loop).
     {
       double X[2][R], G[2][R];
       {
         double H[2][R];
-        st.commit(H);
-        st.prefetch(out[2]);  // H_z
+        st.template commit<0>(H);  // H_x
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           X[0][r] = al * H[1][r];   // -i al Hx
@@ -453,8 +486,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           G[0][r] = is_mean ? H[0][r] : -be * H[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
           G[1][r] = is_mean ? 0.0 : be * H[0][r];
         }
-        st.commit(H);
-        st.prefetch(out[1]);  // H_y
+        st.template commit<1>(H);  // H_z
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           X[0][r] += be * H[1][r];  // -i be Hz
@@ -466,8 +498,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       d1_apply<R, 2>(t, X, lane);  // D(-i al Hx - i be Hz)
       {
         double Hy[2][R];
-        st.commit(Hy);
-        st.prefetch(phi);
+        st.template commit<2>(Hy);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -475,6 +506,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       apply_M<R, 2>(t, X, RPn, lane);
       apply_M<R, 2>(t, G, RWn, lane);
+      KSPEC_STAMP(0)
       if (a.mean_diag && is_mean) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -488,9 +520,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     double rhsP[2][R], rhsW[2][R];
     {
       double q[2][R], Mq[2][R], Kq[2][R];
-      const bool zprev = a.rk_z != 0.0;
-      st.commit(q);
-      st.prefetch(omega);
+      st.template commit<3>(q);  // phi
       apply_M<R, 2>(t, q, Mq, lane);
       apply_K<R, 2>(t, q, Kq, lane);
 #pragma unroll
@@ -498,8 +528,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
           rhsP[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RPn[k][r]);
-      st.commit(q);
-      if (zprev) st.prefetch(Rphi);
+      st.template commit<4>(q);  // omega
       apply_M<R, 2>(t, q, Mq, lane);
       apply_K<R, 2>(t, q, Kq, lane);
 #pragma unroll
@@ -508,21 +537,23 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         for (int r = 0; r < R; ++r)
           rhsW[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RWn[k][r]);
       if (zprev) {
-        st.commit(q);
-        st.prefetch(Romega);
+        st.template commit<5>(q);  // R_phi
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
           for (int r = 0; r < R; ++r) rhsP[k][r] += dt * a.rk_z * q[k][r];
-        st.commit(q);
+        st.template commit<6>(q);  // R_omega
 #pragma unroll
         for (int k = 0; k < 2; ++k)
 #pragma unroll
           for (int r = 0; r < R; ++r) rhsW[k][r] += dt * a.rk_z * q[k][r];
       }
     }
+    KSPEC_STAMP(1)
     st.store(Rphi, RPn);
     st.store(Romega, RWn);
+    KSPEC_STAMP(2)
+    if (has_next) pre_H(next_line0);
 
     // ---------------- implicit viscous solves (phi, omega share one factorisation) ---------
     const double c = a.rk_b * dt * a.nu;
@@ -531,7 +562,31 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       PFac<R> F;
       CoefImpl ci{t, lane, 1.0 + c * k2, c};
       pfactor<R>(F, ci, lane);
-      psolve<R, 2>(F, ci, rhsW, lane);
+      {
+        // omega, phi and the two homogeneous phi solutions share the factorisation: one solve
+        // with 6 real right-hand sides keeps 6 independent chains in flight per PCR level
+        double Z[6][R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = lane * R + r;
+          Z[0][r] = rhsW[0][r];
+          Z[1][r] = rhsW[1][r];
+          Z[2][r] = rhsP[0][r];
+          Z[3][r] = rhsP[1][r];
+          Z[4][r] = (j == 0) ? 1.0 : 0.0;
+          Z[5][r] = (j == N - 1) ? 1.0 : 0.0;
+        }
+        psolve<R, 6>(F, ci, Z, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          rhsW[0][r] = Z[0][r];
+          rhsW[1][r] = Z[1][r];
+          rhsP[0][r] = Z[2][r];
+          rhsP[1][r] = Z[3][r];
+          phH[0][r] = Z[4][r];
+          phH[1][r] = Z[5][r];
+        }
+      }
       if (is_mean) {
         // constant flow rate: U += C * U1, U1 = response to a unit mean pressure gradient
         const double fU = wave_sum<R>([&] {
@@ -567,16 +622,11 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         for (int r = 0; r < R; ++r) rhsW[1][r] = 0.0;
         mean_diag_flux = fU;
       }
-      psolve<R, 2>(F, ci, rhsP, lane);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int j = lane * R + r;
-        phH[0][r] = (j == 0) ? 1.0 : 0.0;
-        phH[1][r] = (j == N - 1) ? 1.0 : 0.0;
-      }
-      psolve<R, 2>(F, ci, phH, lane);
     }
+    KSPEC_STAMP(3)
     st.store(omega, rhsW);
+    KSPEC_STAMP(4)
+    if (has_next) pre_S(next_line0);
 
     // ---------------- velocity recovery + influence matrix (v(+-1) = v'(+-1) = 0) ----------
     {
@@ -584,10 +634,25 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       CoefHelm chm{t, lane, k2};
       pfactor<R>(F, chm, lane);
       double vH[2][R];
-      apply_M<R, 2>(t, rhsP, v, lane);
-      psolve<R, 2>(F, chm, v, lane);
-      apply_M<R, 2>(t, phH, vH, lane);
-      psolve<R, 2>(F, chm, vH, lane);
+      {
+        double Y[4][R], Z[4][R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          Z[0][r] = rhsP[0][r];
+          Z[1][r] = rhsP[1][r];
+          Z[2][r] = phH[0][r];
+          Z[3][r] = phH[1][r];
+        }
+        apply_M<R, 4>(t, Z, Y, lane);
+        psolve<R, 4>(F, chm, Y, lane);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          v[0][r] = Y[0][r];
+          v[1][r] = Y[1][r];
+          vH[0][r] = Y[2][r];
+          vH[1][r] = Y[3][r];
+        }
+      }
       // wall derivatives v'(+-1) = first / last row of the dense D1 applied to v (no solves)
       double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -623,9 +688,12 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         czero<R>(v);
       }
     }
+    KSPEC_STAMP(5)
     // omega was the last field staged (store above): re-read it from the tile, not from HBM
     st.column(om);
     st.store(phi, ph);
+    KSPEC_STAMP(6)
+    if (has_next) pre_R(next_line0);
   } else {
     // ---------------- prepare only: fields from the state ----------------------------------
     st.load(phi, ph);
@@ -650,18 +718,28 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   }
 
   // ---------------- prepare velocity / vorticity for the physical-space stage ----------------
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int r = 0; r < R; ++r) dv[k][r] = v[k][r];
-  d1_apply<R, 2>(t, dv, lane);
   double Dom[2][R];
+  {
+    // D1 of v and omega in one 4-RHS solve
+    double Z[4][R];
 #pragma unroll
-  for (int k = 0; k < 2; ++k)
+    for (int r = 0; r < R; ++r) {
+      Z[0][r] = v[0][r];
+      Z[1][r] = v[1][r];
+      Z[2][r] = om[0][r];
+      Z[3][r] = om[1][r];
+    }
+    d1_apply<R, 4>(t, Z, lane);
 #pragma unroll
-    for (int r = 0; r < R; ++r) Dom[k][r] = om[k][r];
-  d1_apply<R, 2>(t, Dom, lane);
+    for (int r = 0; r < R; ++r) {
+      dv[0][r] = Z[0][r];
+      dv[1][r] = Z[1][r];
+      Dom[0][r] = Z[2][r];
+      Dom[1][r] = Z[3][r];
+    }
+  }
 
+  KSPEC_STAMP(7)
   double fu[2][R], fw[2][R];
   // u = i (al dv - be om)/k2 ; w = i (be dv + al om)/k2   (nonLinear_kernels.cu:55-72)
 #pragma unroll
@@ -703,7 +781,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
     }
   }
-  if (a.mode == 1 && next_line0 < a.lines) st.prefetch_at(out[0], next_line0);  // next tile's H_x
+  KSPEC_STAMP(8)
   st.store(out[0], fu);
   st.store(out[1], v);
   st.store(out[2], fw);
@@ -756,7 +834,11 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       a.mean_diag[3 * N + 3] = mean_C;
     }
   }
+  KSPEC_STAMP(9)
   }  // tile loop
+#undef KSPEC_STAMP
+  if (prof_on && lane == 0)
+    for (int k = 0; k < kKspecPhases; ++k) atomicAdd(&a.prof[k], pacc[k]);
 }
 
 template <int R, typename T>
