@@ -35,6 +35,8 @@ def main() -> None:
     ap.add_argument("--grid", default="1024x385x1024", help="NX x NY x Nz_physical")
     ap.add_argument("--re", type=float, default=20700.0, help="1/nu (Re_tau~950 at Q=1.8, SURVEY App. C)")
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--decomposition", default="slab", choices=["slab", "pencil"])
+    ap.add_argument("--pr", type=int, default=0, help="pencil rows (0 = automatic, most square)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--phases", action="store_true", help="per-phase timing (eager, synchronising)")
     args = ap.parse_args()
@@ -53,7 +55,7 @@ def main() -> None:
     NX, NY, NZP = (int(v) for v in args.grid.lower().split("x"))
     cfg = default_config(NX=NX, NY=NY, NZ=NZP // 2 + 1, Re=args.re, precision=args.precision, ic="random",
                          ic_amplitude=0.05, stats_every=0, log_every=0, symmetry_every=0, checkpoint_every=0,
-                         health_check=True)
+                         health_check=True, decomposition=args.decomposition, pr=args.pr)
     uid = nccl_unique_id()
     solver = C.Solver(cfg, rank, world, torch.cuda.current_device(), uid)
     if args.no_graph:
@@ -107,7 +109,8 @@ def main() -> None:
             "grid": f"{NX}x{NY}x{NZP}",
             "global_batch": 1,
             "seq_len": pts,
-            "parallelism": f"slab{world}",
+            "parallelism": (f"slab{world}" if solver.plan.Pr == 1
+                            else f"pencil{solver.plan.Pr}x{solver.plan.Pc}"),
             "hipgraph": not args.no_graph,
         },
         "health": int(L.health),

@@ -59,3 +59,59 @@ class SlabDecomposition:
             b = sum(x for q, x in enumerate(self.a2a_backward_bytes(r, esz)) if q != r)
             worst = max(worst, b)
         return 3 * 9 * worst
+
+
+def auto_pencil_grid(P: int) -> tuple[int, int]:
+    """Most square Pr x Pc with Pr <= Pc (Plan::auto_grid)."""
+    pr = max(r for r in range(1, int(P ** 0.5) + 1) if P % r == 0)
+    return pr, P // pr
+
+
+@dataclasses.dataclass(frozen=True)
+class PencilDecomposition:
+    """Pr x Pc pencil grid (Python mirror of Plan for decomposition = "pencil").
+
+    rank = prow * Pc + pcol.  Spectral [y][kx in KX_pcol][kz in KZ_prow]; the A exchange
+    (column group, Pc ranks) swaps kx <-> y, the B exchange (row group, Pr ranks) swaps kz <-> x;
+    the z stage sees [y in Y_pcol][x in X_prow][kz (all)].  Pr = 1 is the slab.
+    """
+    NX: int
+    NY: int
+    NZ: int
+    Pr: int
+    Pc: int
+
+    @property
+    def P(self) -> int:
+        return self.Pr * self.Pc
+
+    @property
+    def nkx(self) -> int:
+        return 2 * (self.NX // 3) + 1
+
+    @property
+    def nkz(self) -> int:
+        return (2 * self.NZ - 2) // 3 + 1
+
+    def coords(self, rank: int) -> tuple[int, int]:
+        return divmod(rank, self.Pc)
+
+    def local(self, rank: int) -> dict:
+        prow, pcol = self.coords(rank)
+        ks, kc = balanced_split(self.nkx, self.Pc)
+        ys, yc = balanced_split(self.NY, self.Pc)
+        zs, zc = balanced_split(self.nkz, self.Pr)
+        xs, xc = balanced_split(self.NX, self.Pr)
+        return dict(kx0=ks[pcol], nkx_loc=kc[pcol], y0=ys[pcol], ny_loc=yc[pcol], kz0=zs[prow], nkz_loc=zc[prow],
+                    x0=xs[prow], nx_loc=xc[prow])
+
+    def exchange_bytes_per_substep(self, rank: int, esz: int = 8) -> dict:
+        """off-rank bytes sent by ``rank`` per substep: A (6 backward + 3 forward fields over the
+        column group) and B (6 + 3 over the row group; 0 for the slab)."""
+        L = self.local(rank)
+        prow, pcol = self.coords(rank)
+        ys, yc = balanced_split(self.NY, self.Pc)
+        xs, xc = balanced_split(self.NX, self.Pr)
+        a = sum(yc[c] for c in range(self.Pc) if c != pcol) * L["nkx_loc"] * L["nkz_loc"] * esz
+        b = sum(xc[r] for r in range(self.Pr) if r != prow) * L["ny_loc"] * L["nkz_loc"] * esz
+        return {"A": 9 * a, "B": 9 * b}

@@ -203,6 +203,11 @@ def balanced_split(n: int, parts: int) -> tuple[list[int], list[int]]:
 
 @dataclasses.dataclass
 class OraclePlan:
+    """Decomposition of the retained modes over P = Pr x Pc ranks (rank = prow * Pc + pcol).
+
+    Slab (Pr = 1): kx split over P, physical y split over P.  Pencil (Pr > 1): kx and y split
+    over the Pc columns, kz and physical x split over the Pr rows (csrc/include/channel/plan.hpp).
+    """
     NX: int
     NY: int
     NZ: int
@@ -210,6 +215,7 @@ class OraclePlan:
     rank: int = 0
     LX: float = 2 * math.pi
     LZ: float = math.pi
+    Pr: int = 1
 
     def __post_init__(self):
         self.Nzp = 2 * self.NZ - 2
@@ -217,12 +223,23 @@ class OraclePlan:
         self.nkx = 2 * self.Kx + 1
         self.Kz = self.Nzp // 3
         self.nkz = self.Kz + 1
-        self.kx_start, self.kx_count = balanced_split(self.nkx, self.P)
-        self.y_start, self.y_count = balanced_split(self.NY, self.P)
-        self.kx0, self.nkx_loc = self.kx_start[self.rank], self.kx_count[self.rank]
-        self.y0, self.ny_loc = self.y_start[self.rank], self.y_count[self.rank]
+        if self.P % self.Pr:
+            raise ValueError(f"Pr={self.Pr} does not divide P={self.P}")
+        self.Pc = self.P // self.Pr
+        self.prow, self.pcol = divmod(self.rank, self.Pc)
+        self.kx_start, self.kx_count = balanced_split(self.nkx, self.Pc)
+        self.y_start, self.y_count = balanced_split(self.NY, self.Pc)
+        self.kz_start, self.kz_count = balanced_split(self.nkz, self.Pr)
+        self.x_start, self.x_count = balanced_split(self.NX, self.Pr)
+        self.kx0, self.nkx_loc = self.kx_start[self.pcol], self.kx_count[self.pcol]
+        self.y0, self.ny_loc = self.y_start[self.pcol], self.y_count[self.pcol]
+        self.kz0, self.nkz_loc = self.kz_start[self.prow], self.kz_count[self.prow]
+        self.x0, self.nx_loc = self.x_start[self.prow], self.x_count[self.prow]
         self.ax = 2 * math.pi / self.LX
         self.az = 2 * math.pi / self.LZ
+
+    def rank_of(self, row: int, col: int) -> int:
+        return row * self.Pc + col
 
     def kx_of(self, i: np.ndarray | int):
         i = np.asarray(i)
@@ -235,8 +252,8 @@ class OraclePlan:
     def local_wavenumbers(self):
         ig = self.kx0 + np.arange(self.nkx_loc)
         kx = self.kx_of(ig).astype(float)
-        kz = np.arange(self.nkz, dtype=float)
-        al = self.ax * np.repeat(kx, self.nkz)
+        kz = self.kz0 + np.arange(self.nkz_loc, dtype=float)
+        al = self.ax * np.repeat(kx, self.nkz_loc)
         be = self.az * np.tile(kz, self.nkx_loc)
         return al, be
 
@@ -275,14 +292,14 @@ class OracleSolver:
     """
 
     def __init__(self, NX, NY, NZ, Re=3250.0, Q=1.8, LX=2 * math.pi, LZ=math.pi, stretch=2.0, cfl=0.5,
-                 dt_max=0.05, dt_fixed=0.0, P=1, rank=0, dist=None):
-        self.plan = OraclePlan(NX, NY, NZ, P, rank, LX, LZ)
+                 dt_max=0.05, dt_fixed=0.0, P=1, rank=0, dist=None, Pr=1):
+        self.plan = OraclePlan(NX, NY, NZ, P, rank, LX, LZ, Pr)
         self.ops = build_ops(NY, stretch)
         self.Re, self.nu, self.Q = Re, 1.0 / Re, Q
         self.cfl, self.dt_max, self.dt_fixed = cfl, dt_max, dt_fixed
         self.dist = dist
         p = self.plan
-        shape = (NY, p.nkx_loc, p.nkz)
+        shape = (NY, p.nkx_loc, p.nkz_loc)
         self.phi = np.zeros(shape, complex)
         self.om = np.zeros(shape, complex)
         self.Rphi = np.zeros(shape, complex)
@@ -294,7 +311,7 @@ class OracleSolver:
         self.maxima = np.zeros(4)
         al, be = p.local_wavenumbers()
         self.al, self.be, self.k2 = al, be, al * al + be * be
-        self.mean_line = 0 if (p.kx0 == 0) else None
+        self.mean_line = 0 if (p.kx0 == 0 and p.kz0 == 0) else None
         self.fields = None              # 6 prepared fields [6, y, nkx_loc, nkz]
         y = self.ops.y
         h = np.empty(NY)
@@ -351,16 +368,21 @@ class OracleSolver:
         self.fields = self._prepare(phi_l, om_l, v_l, self.U)
 
     # ---- physical stage (optionally distributed) ----------------------------------------------
-    def _a2a(self, blocks_send):
+    def _a2a(self, send: dict, recv_shapes: dict):
+        """Variable all-to-all on the world group; peers missing from ``send``/``recv_shapes``
+        exchange nothing (the pencil row/column exchanges, like the GPU's alltoallv)."""
         import torch
         import torch.distributed as dist
 
-        send = [torch.from_numpy(np.ascontiguousarray(b).view(np.float64)).reshape(-1) for b in blocks_send]
-        in_splits = [t.numel() for t in send]
-        out_splits = list(self._recv_sizes)
+        P = self.plan.P
+        flat = [torch.from_numpy(np.ascontiguousarray(send[g]).view(np.float64)).reshape(-1) if g in send
+                else torch.zeros(0, dtype=torch.float64) for g in range(P)]
+        in_splits = [t.numel() for t in flat]
+        out_splits = [2 * int(np.prod(recv_shapes[g])) if g in recv_shapes else 0 for g in range(P)]
         out = torch.empty(sum(out_splits), dtype=torch.float64)
-        dist.all_to_all_single(out, torch.cat(send), out_splits, in_splits, group=self.dist)
-        return [t.numpy() for t in torch.split(out, out_splits)]
+        dist.all_to_all_single(out, torch.cat(flat), out_splits, in_splits, group=self.dist)
+        parts = torch.split(out, out_splits)
+        return {g: parts[g].numpy().view(complex).reshape(recv_shapes[g]) for g in recv_shapes}
 
     def transforms(self, compute_dt: bool):
         p = self.plan
@@ -371,20 +393,29 @@ class OracleSolver:
             self._maxima(phys, p.y0)
             self.H = phys_to_spec_full(H, p)
         else:
-            # backward: send rows y in Y_q of my kx slab to rank q
-            blocks = [F[:, p.y_start[q]:p.y_start[q] + p.y_count[q]] for q in range(p.P)]
-            self._recv_sizes = [2 * 6 * p.ny_loc * p.kx_count[q] * p.nkz for q in range(p.P)]
-            recv = self._a2a(blocks)
-            parts = [r.view(complex).reshape(6, p.ny_loc, p.kx_count[q], p.nkz) for q, r in enumerate(recv)]
-            full = np.concatenate(parts, axis=2)  # [6, ny_loc, nkx, nkz]
-            phys = spec_to_phys_full(full, p)
+            cols = [p.rank_of(p.prow, c) for c in range(p.Pc)]   # A exchange: kx <-> y
+            rows = [p.rank_of(r, p.pcol) for r in range(p.Pr)]   # B exchange: kz <-> x
+            nf = F.shape[0]
+            recv = self._a2a({g: F[:, p.y_start[c]:p.y_start[c] + p.y_count[c]] for c, g in enumerate(cols)},
+                             {g: (nf, p.ny_loc, p.kx_count[c], p.nkz_loc) for c, g in enumerate(cols)})
+            full = np.concatenate([recv[g] for g in cols], axis=2)  # [6, ny_loc, nkx, nkz_loc]
+            X = np.zeros(full.shape[:2] + (p.NX, p.nkz_loc), complex)
+            X[:, :, p.kx_pos(np.arange(p.nkx))] = full
+            X = np.fft.ifft(X, axis=2, norm="forward")             # [6, ny_loc, NX, nkz_loc]
+            recv = self._a2a({g: X[:, :, p.x_start[r]:p.x_start[r] + p.x_count[r]] for r, g in enumerate(rows)},
+                             {g: (nf, p.ny_loc, p.nx_loc, p.kz_count[r]) for r, g in enumerate(rows)})
+            Z = np.zeros((nf, p.ny_loc, p.nx_loc, p.NZ), complex)
+            Z[..., :p.nkz] = np.concatenate([recv[g] for g in rows], axis=3)
+            phys = np.fft.irfft(Z, n=p.Nzp, axis=-1, norm="forward")  # [6, ny_loc, nx_loc, Nzp]
             self._maxima(phys, p.y0)
-            Hs = phys_to_spec_full(rotational_product(phys), p)  # [3, ny_loc, nkx, nkz]
-            blocks = [Hs[:, :, p.kx_start[q]:p.kx_start[q] + p.kx_count[q]] for q in range(p.P)]
-            self._recv_sizes = [2 * 3 * p.y_count[q] * p.nkx_loc * p.nkz for q in range(p.P)]
-            recv = self._a2a(blocks)
-            parts = [r.view(complex).reshape(3, p.y_count[q], p.nkx_loc, p.nkz) for q, r in enumerate(recv)]
-            self.H = np.concatenate(parts, axis=1)
+            Hk = np.fft.rfft(rotational_product(phys), axis=-1, norm="forward")[..., :p.nkz]
+            recv = self._a2a({g: Hk[..., p.kz_start[r]:p.kz_start[r] + p.kz_count[r]] for r, g in enumerate(rows)},
+                             {g: (3, p.ny_loc, p.x_count[r], p.nkz_loc) for r, g in enumerate(rows)})
+            Xh = np.fft.fft(np.concatenate([recv[g] for g in rows], axis=2), axis=2, norm="forward")
+            Hs = Xh[:, :, p.kx_pos(np.arange(p.nkx))]              # [3, ny_loc, nkx, nkz_loc]
+            recv = self._a2a({g: Hs[:, :, p.kx_start[c]:p.kx_start[c] + p.kx_count[c]] for c, g in enumerate(cols)},
+                             {g: (3, p.y_count[c], p.nkx_loc, p.nkz_loc) for c, g in enumerate(cols)})
+            self.H = np.concatenate([recv[g] for g in cols], axis=1)
             if compute_dt:
                 import torch
                 import torch.distributed as dist
@@ -496,7 +527,7 @@ class OracleSolver:
         """[4, NY]: <u'u'>, <v'v'>, <w'w'>, <u'v'> (plane averages, fluctuations only)."""
         p = self.plan
         u, v, w = (self.lines(f) for f in self.fields[:3])
-        wgt = np.where(np.tile(np.arange(p.nkz), p.nkx_loc) == 0, 1.0, 2.0)
+        wgt = np.where(np.tile(p.kz0 + np.arange(p.nkz_loc), p.nkx_loc) == 0, 1.0, 2.0)
         if self.mean_line is not None:
             wgt = wgt.copy()
             wgt[self.mean_line] = 0

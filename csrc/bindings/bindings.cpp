@@ -165,7 +165,7 @@ torch::Tensor field_tensor(Solver& s, int f) {
   auto opts = torch::TensorOptions()
                   .dtype(s.fp64() ? torch::kComplexDouble : torch::kComplexFloat)
                   .device(torch::kCUDA, c10::hip::current_device());
-  return torch::from_blob(s.field_ptr(f), {p.NY, p.nkx_loc, p.nkz}, opts);
+  return torch::from_blob(s.field_ptr(f), {p.NY, p.nkx_loc, p.nkz_loc}, opts);
 }
 
 torch::Tensor phys_tensor(Solver& s) {
@@ -173,7 +173,7 @@ torch::Tensor phys_tensor(Solver& s) {
   auto opts = torch::TensorOptions()
                   .dtype(s.fp64() ? torch::kComplexDouble : torch::kComplexFloat)
                   .device(torch::kCUDA, c10::hip::current_device());
-  return torch::from_blob(s.phys_ptr(), {6, p.ny_loc, p.NX, p.nkz}, opts);
+  return torch::from_blob(s.phys_ptr(), {6, p.ny_loc, p.NX, p.nkz_loc}, opts);
 }
 
 }  // namespace
@@ -242,9 +242,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_static("make", &Plan::make)
 #define RO(f) .def_readonly(#f, &Plan::f)
       RO(NX) RO(NY) RO(NZ) RO(Nzp) RO(Kx) RO(nkx) RO(Kz) RO(nkz) RO(P) RO(rank) RO(kx_split) RO(y_split) RO(nkx_loc)
-      RO(kx0) RO(ny_loc) RO(y0) RO(R) RO(ax) RO(az)
+      RO(kx0) RO(ny_loc) RO(y0) RO(R) RO(ax) RO(az) RO(Pr) RO(Pc) RO(prow) RO(pcol) RO(kz_split) RO(x_split)
+      RO(nkz_loc) RO(kz0) RO(nx_loc) RO(x0)
 #undef RO
       .def("lines_loc", &Plan::lines_loc)
+      .def("pencil", &Plan::pencil)
+      .def("owns_mean", &Plan::owns_mean)
       .def("kx_of", &Plan::kx_of)
       .def("kx_fft_pos", &Plan::kx_fft_pos);
 
@@ -295,7 +298,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
               py::array_t<double, py::array::c_style | py::array::forcecast> U) {
              const size_t n = s.plan().spec_elems();
              TORCH_CHECK(static_cast<size_t>(phi.size()) == n && static_cast<size_t>(om.size()) == n,
-                         "state arrays must have NY*nkx_loc*nkz elements");
+                         "state arrays must have NY*nkx_loc*nkz_loc elements");
              TORCH_CHECK(U.size() == s.plan().NY, "U must have NY elements");
              py::gil_scoped_release r;
              s.set_state(phi.data(), om.data(), U.data());
@@ -303,7 +306,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("get_state",
            [](Solver& s) {
              const Plan& p = s.plan();
-             py::array_t<std::complex<double>> phi({p.NY, p.nkx_loc, p.nkz}), om({p.NY, p.nkx_loc, p.nkz});
+             py::array_t<std::complex<double>> phi({p.NY, p.nkx_loc, p.nkz_loc}), om({p.NY, p.nkx_loc, p.nkz_loc});
              py::array_t<double> U(p.NY);
              s.get_state(phi.mutable_data(), om.mutable_data(), U.mutable_data());
              return py::make_tuple(phi, om, U);

@@ -29,6 +29,13 @@ int Split::owner(int idx) const {
   return 0;
 }
 
+void Plan::auto_grid(int P, int& Pr, int& Pc) {
+  Pr = 1;
+  for (int r = 1; r * r <= P; ++r)
+    if (P % r == 0) Pr = r;
+  Pc = P / Pr;
+}
+
 int Split::max_count() const { return *std::max_element(count.begin(), count.end()); }
 
 Plan Plan::make(const Config& cfg, int P, int rank) {
@@ -46,13 +53,37 @@ Plan Plan::make(const Config& cfg, int P, int rank) {
   p.P = P;
   p.rank = rank;
   CH_CHECK(rank >= 0 && rank < P, "bad rank " << rank << " of " << P);
-  CH_CHECK(P <= p.nkx && P <= p.NY, "P=" << P << " exceeds retained kx (" << p.nkx << ") or NY (" << p.NY << ")");
-  p.kx_split = Split::balanced(p.nkx, P);
-  p.y_split = Split::balanced(p.NY, P);
-  p.nkx_loc = p.kx_split.count[rank];
-  p.kx0 = p.kx_split.start[rank];
-  p.ny_loc = p.y_split.count[rank];
-  p.y0 = p.y_split.start[rank];
+  if (cfg.decomposition == "pencil") {
+    if (cfg.pr > 0 || cfg.pc > 0) {
+      p.Pr = cfg.pr > 0 ? cfg.pr : P / std::max(1, cfg.pc);
+      p.Pc = cfg.pc > 0 ? cfg.pc : P / std::max(1, cfg.pr);
+    } else {
+      auto_grid(P, p.Pr, p.Pc);
+    }
+    CH_CHECK(p.Pr * p.Pc == P, "pencil grid pr x pc = " << p.Pr << " x " << p.Pc << " does not match " << P << " ranks");
+  } else {
+    p.Pr = 1;
+    p.Pc = P;
+  }
+  CH_CHECK(p.Pc <= 8 && p.Pr <= 8, "each exchange group holds at most 8 ranks (pr, pc <= 8)");
+  CH_CHECK(p.Pc <= p.nkx && p.Pc <= p.NY,
+           "pc=" << p.Pc << " exceeds retained kx (" << p.nkx << ") or NY (" << p.NY << ")");
+  CH_CHECK(p.Pr <= p.nkz && p.Pr <= p.NX,
+           "pr=" << p.Pr << " exceeds retained kz (" << p.nkz << ") or NX (" << p.NX << ")");
+  p.prow = rank / p.Pc;
+  p.pcol = rank % p.Pc;
+  p.kx_split = Split::balanced(p.nkx, p.Pc);
+  p.y_split = Split::balanced(p.NY, p.Pc);
+  p.kz_split = Split::balanced(p.nkz, p.Pr);
+  p.x_split = Split::balanced(p.NX, p.Pr);
+  p.nkx_loc = p.kx_split.count[p.pcol];
+  p.kx0 = p.kx_split.start[p.pcol];
+  p.ny_loc = p.y_split.count[p.pcol];
+  p.y0 = p.y_split.start[p.pcol];
+  p.nkz_loc = p.kz_split.count[p.prow];
+  p.kz0 = p.kz_split.start[p.prow];
+  p.nx_loc = p.x_split.count[p.prow];
+  p.x0 = p.x_split.start[p.prow];
   p.R = (p.NY + 63) / 64;
   CH_CHECK(p.R <= 16, "NY too large for the y-line solver (max 1024)");
   const double two_pi = 2.0 * std::acos(-1.0);

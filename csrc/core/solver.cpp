@@ -87,7 +87,6 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
     // grid sizes); capturing RCCL into the step graph is opt-in (CHANNEL_GRAPH_MULTI=1).
     const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
     if (!comm_->graph_capturable() || !(gm && std::atoi(gm) == 1)) use_graph_ = false;
-    CH_CHECK(nranks <= 8, "slab decomposition supports P <= 8 ranks per job in this version");
   }
   ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
   tw_x_.build(plan_.NX, fp64_);
@@ -111,7 +110,8 @@ void Solver::alloc() {
   const Plan& p = plan_;
   spec_ = p.spec_elems();
   physn_ = p.phys_elems();
-  xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz;
+  xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz_loc;
+  zstride_ = p.pencil() ? p.zrow_elems() : 0;
   HIP_CHECK(hipMalloc(&state_, 4 * spec_ * esz_));
   HIP_CHECK(hipMalloc(&out_, 6 * spec_ * esz_));
   HIP_CHECK(hipMalloc(&phys_, std::max<size_t>(6 * physn_, 1) * esz_));
@@ -120,6 +120,10 @@ void Solver::alloc() {
   if (p.P > 1) {
     HIP_CHECK(hipMalloc(&xbuf_, 6 * xstride_ * esz_));
     HIP_CHECK(hipMemset(xbuf_, 0, 6 * xstride_ * esz_));
+  }
+  if (p.pencil()) {
+    HIP_CHECK(hipMalloc(&zbuf_, 6 * zstride_ * esz_));
+    HIP_CHECK(hipMemset(zbuf_, 0, 6 * zstride_ * esz_));
   }
   const int N = p.NY;
   // scalars: dt, time, dtlog[8], stats[4N], mean[3N+8], invdy[N], maxima[4] (float), health
@@ -146,9 +150,11 @@ void Solver::alloc() {
   }
   HIP_CHECK(hipMemcpy(d_invdy_, invdy.data(), N * sizeof(double), hipMemcpyHostToDevice));
   ev_a2a_.resize(6);
-  ev_xf_.resize(3);
-  for (auto& e : ev_a2a_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (auto& e : ev_xf_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  ev_xf_.resize(6);
+  ev_b_.resize(6);
+  ev_bb_.resize(3);
+  for (auto* v : {&ev_a2a_, &ev_xf_, &ev_b_, &ev_bb_})
+    for (auto& e : *v) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_spec_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_phys_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_fwd_done_, hipEventDisableTiming));
@@ -162,14 +168,14 @@ void Solver::alloc() {
 void Solver::free_all() {
   for (int i = 0; i < 2; ++i)
     if (gexec_[i]) (void)hipGraphExecDestroy(gexec_[i]);
-  for (auto e : ev_a2a_) (void)hipEventDestroy(e);
-  for (auto e : ev_xf_) (void)hipEventDestroy(e);
+  for (auto* v : {&ev_a2a_, &ev_xf_, &ev_b_, &ev_bb_})
+    for (auto e : *v) (void)hipEventDestroy(e);
   for (auto e : ph_ev_) (void)hipEventDestroy(e);
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
     if (e) (void)hipEventDestroy(e);
-  for (void* p : {state_, out_, phys_, xbuf_, dscal_})
+  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_})
     if (p) (void)hipFree(p);
-  state_ = out_ = phys_ = xbuf_ = dscal_ = nullptr;
+  state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = nullptr;
 }
 
 void* Solver::field_ptr(int f) const {
@@ -251,8 +257,9 @@ void Solver::init_ic() {
     for (int ikx = 0; ikx < p.nkx_loc; ++ikx) {
       const int ig = p.kx0 + ikx;
       const int kx = p.kx_of(ig);
-      for (int kz = 0; kz < p.nkz; ++kz) {
-        const int line = ikx * p.nkz + kz;
+      for (int kzl = 0; kzl < p.nkz_loc; ++kzl) {
+        const int kz = p.kz0 + kzl;
+        const int line = ikx * p.nkz_loc + kzl;
         if (kx == 0 && kz == 0) continue;
         const double al = p.ax * kx, be = p.az * kz, k2 = al * al + be * be;
         const double env = std::exp(-k2 / 32.0);
@@ -309,7 +316,8 @@ void Solver::kspec(int mode, int n, bool stats) {
   SpecArgs a;
   a.N = p.NY;
   a.lines = p.lines_loc();
-  a.nkz = p.nkz;
+  a.nkz = p.nkz_loc;
+  a.kz0 = p.kz0;
   a.kx0 = p.kx0;
   a.nkx = p.nkx;
   a.Kx = p.Kx;
@@ -348,34 +356,42 @@ void Solver::kspec(int mode, int n, bool stats) {
   }
 }
 
-void Solver::a2a_backward(int f) {
+// A exchange (column group: the Pc ranks of this process row), kx <-> y.
+// spectral [y][kx_loc][kz_loc]: the block for column c is the contiguous row range Y_c;
+// received blocks are [src column][y_loc][nkx_src][kz_loc] (the x transform gathers from them).
+void Solver::a2a_spec(const void* spec, void* xb, bool to_phys) {
   const Plan& p = plan_;
-  const int P = p.P, lines = p.lines_loc();
-  std::vector<size_t> sc(P), so(P), rc(P), ro(P);
-  for (int q = 0; q < P; ++q) {
-    so[q] = static_cast<size_t>(p.y_split.start[q]) * lines * esz_;
-    sc[q] = static_cast<size_t>(p.y_split.count[q]) * lines * esz_;
-    ro[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.start[q] * p.nkz * esz_;
-    rc[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.count[q] * p.nkz * esz_;
+  const int lines = p.lines_loc();
+  std::vector<size_t> sc(p.P, 0), so(p.P, 0), rc(p.P, 0), ro(p.P, 0);
+  for (int c = 0; c < p.Pc; ++c) {
+    const int g = p.rank_of(p.prow, c);
+    const size_t yo = static_cast<size_t>(p.y_split.start[c]) * lines * esz_;
+    const size_t yc = static_cast<size_t>(p.y_split.count[c]) * lines * esz_;
+    const size_t xo = static_cast<size_t>(p.ny_loc) * p.kx_split.start[c] * p.nkz_loc * esz_;
+    const size_t xc = static_cast<size_t>(p.ny_loc) * p.kx_split.count[c] * p.nkz_loc * esz_;
+    if (to_phys) { so[g] = yo; sc[g] = yc; ro[g] = xo; rc[g] = xc; }
+    else { so[g] = xo; sc[g] = xc; ro[g] = yo; rc[g] = yc; }
   }
-  const char* send = static_cast<const char*>(field_ptr(OUT0 + f));
-  char* recv = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-  comm_->alltoallv(send, sc, so, recv, rc, ro, s_comm_);
+  if (to_phys) comm_->alltoallv(spec, sc, so, xb, rc, ro, s_comm_);
+  else comm_->alltoallv(xb, sc, so, const_cast<void*>(spec), rc, ro, s_comm_);
 }
 
-void Solver::a2a_forward(int f) {
+// B exchange (row group: the Pr ranks of this process column), kz <-> x (pencil only).
+// x-expanded [dst row][y_loc][x_r][kz_loc] <-> z rows [src row][y_loc][x_loc][kz_r].
+void Solver::a2a_rows(void* xexp, void* zrows, bool to_z) {
   const Plan& p = plan_;
-  const int P = p.P, lines = p.lines_loc();
-  std::vector<size_t> sc(P), so(P), rc(P), ro(P);
-  for (int q = 0; q < P; ++q) {
-    so[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.start[q] * p.nkz * esz_;
-    sc[q] = static_cast<size_t>(p.ny_loc) * p.kx_split.count[q] * p.nkz * esz_;
-    ro[q] = static_cast<size_t>(p.y_split.start[q]) * lines * esz_;
-    rc[q] = static_cast<size_t>(p.y_split.count[q]) * lines * esz_;
+  std::vector<size_t> sc(p.P, 0), so(p.P, 0), rc(p.P, 0), ro(p.P, 0);
+  for (int r = 0; r < p.Pr; ++r) {
+    const int g = p.rank_of(r, p.pcol);
+    const size_t xo = static_cast<size_t>(p.ny_loc) * p.x_split.start[r] * p.nkz_loc * esz_;
+    const size_t xc = static_cast<size_t>(p.ny_loc) * p.x_split.count[r] * p.nkz_loc * esz_;
+    const size_t zo = static_cast<size_t>(p.ny_loc) * p.nx_loc * p.kz_split.start[r] * esz_;
+    const size_t zc = static_cast<size_t>(p.ny_loc) * p.nx_loc * p.kz_split.count[r] * esz_;
+    if (to_z) { so[g] = xo; sc[g] = xc; ro[g] = zo; rc[g] = zc; }
+    else { so[g] = zo; sc[g] = zc; ro[g] = xo; rc[g] = xc; }
   }
-  const char* send = static_cast<const char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-  char* recv = static_cast<char*>(field_ptr(OUT0 + f));
-  comm_->alltoallv(send, sc, so, recv, rc, ro, s_comm_);
+  if (to_z) comm_->alltoallv(xexp, sc, so, zrows, rc, ro, s_comm_);
+  else comm_->alltoallv(zrows, sc, so, xexp, rc, ro, s_comm_);
 }
 
 void Solver::ev(int phase, bool end) {
@@ -461,34 +477,69 @@ void Solver::transforms(int n, bool /*stats*/) {
     ev(3, true);
     return;
   }
-  // ---- P > 1: per-field all-to-all on the comm stream, overlapped with the x transforms ----
-  const int P = p.P;
+  // ---- P > 1: per-field exchanges on the comm stream, overlapped with the x transforms ----
+  const int Pc = p.Pc, Pr = p.Pr;
+  const bool pen = p.pencil();
   XSrc src;
   src.base = xbuf_;
-  src.nsrc = P;
+  src.nsrc = Pc;
   XDst dst;
   dst.base = xbuf_;
-  dst.ndst = P;
-  for (int q = 0; q < P; ++q) {
-    src.kx_start[q] = dst.kx_start[q] = p.kx_split.start[q];
-    src.off[q] = dst.off[q] = static_cast<long long>(p.ny_loc) * p.kx_split.start[q] * p.nkz;
+  dst.ndst = Pc;
+  for (int c = 0; c < Pc; ++c) {
+    src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
+    src.off[c] = dst.off[c] = static_cast<long long>(p.ny_loc) * p.kx_split.start[c] * p.nkz_loc;
   }
-  src.kx_start[P] = dst.kx_start[P] = p.nkx;
+  src.kx_start[Pc] = dst.kx_start[Pc] = p.nkx;
+  xa.nkz = p.nkz_loc;
   xa.nfields = 1;
   xa.field_stride_spec = static_cast<long long>(xstride_);
+  if (pen) {  // x-expanded output blocked by destination row (x range)
+    xa.npseg = Pr;
+    for (int r = 0; r < Pr; ++r) {
+      xa.x_start[r] = p.x_split.start[r];
+      xa.poff[r] = static_cast<long long>(p.ny_loc) * p.x_split.start[r] * p.nkz_loc;
+    }
+    xa.x_start[Pr] = p.NX;
+    // z stage over [src row][y_loc][x_loc][kz_r]
+    za.NX = p.nx_loc;
+    za.field_stride = static_cast<long long>(zstride_);
+    za.nseg = Pr;
+    for (int r = 0; r < Pr; ++r) {
+      za.kz_start[r] = p.kz_split.start[r];
+      za.off[r] = static_cast<long long>(p.ny_loc) * p.nx_loc * p.kz_split.start[r];
+    }
+    za.kz_start[Pr] = p.nkz;
+  }
+  auto fld = [&](void* base, size_t stride, int f) { return static_cast<char*>(base) + static_cast<size_t>(f) * stride * esz_; };
   HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
   HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
   for (int f = 0; f < 6; ++f) {
-    a2a_backward(f);
+    a2a_spec(field_ptr(OUT0 + f), fld(xbuf_, xstride_, f), true);
     HIP_CHECK(hipEventRecord(ev_a2a_[f], s_comm_));
   }
+  ev(1, false);
   for (int f = 0; f < 6; ++f) {
     HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_a2a_[f], 0));
     XSrc sf = src;
-    sf.base = static_cast<const char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-    xfft_backward(xa, sf, static_cast<char*>(phys_) + static_cast<size_t>(f) * physn_ * esz_, tw_x_, fp64_, s_comp_);
+    sf.base = fld(xbuf_, xstride_, f);
+    xfft_backward(xa, sf, fld(phys_, physn_, f), tw_x_, fp64_, s_comp_);
+    if (pen) {  // ship field f's x-blocks to the row group while field f+1 is transformed
+      HIP_CHECK(hipEventRecord(ev_b_[f], s_comp_));
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_b_[f], 0));
+      a2a_rows(fld(phys_, physn_, f), fld(zbuf_, zstride_, f), true);
+    }
   }
-  zphys(za, phys_, tw_z_, fp64_, s_comp_);
+  ev(1, true);
+  void* zf = phys_;
+  if (pen) {
+    HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+    zf = zbuf_;
+  }
+  ev(2, false);
+  zphys(za, zf, tw_z_, fp64_, s_comp_);
+  ev(2, true);
   if (n == 0) {
     HIP_CHECK(hipEventRecord(ev_phys_, s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_phys_, 0));
@@ -497,14 +548,25 @@ void Solver::transforms(int n, bool /*stats*/) {
     HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_red_, 0));
     dt_update(da, s_comp_);
   }
+  if (pen) {
+    HIP_CHECK(hipEventRecord(ev_phys_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_phys_, 0));
+    for (int f = 0; f < 3; ++f) {
+      a2a_rows(fld(phys_, physn_, f), fld(zbuf_, zstride_, f), false);
+      HIP_CHECK(hipEventRecord(ev_bb_[f], s_comm_));
+    }
+  }
+  ev(3, false);
   for (int f = 0; f < 3; ++f) {
+    if (pen) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bb_[f], 0));
     XDst df = dst;
-    df.base = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-    xfft_forward(xa, static_cast<char*>(phys_) + static_cast<size_t>(f) * physn_ * esz_, df, tw_x_, fp64_, s_comp_);
+    df.base = fld(xbuf_, xstride_, f);
+    xfft_forward(xa, fld(phys_, physn_, f), df, tw_x_, fp64_, s_comp_);
     HIP_CHECK(hipEventRecord(ev_xf_[f], s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_xf_[f], 0));
-    a2a_forward(f);
+    a2a_spec(field_ptr(OUT0 + f), fld(xbuf_, xstride_, f), false);
   }
+  ev(3, true);
   HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
   HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
 }
@@ -765,17 +827,16 @@ void Solver::write_restart(const std::string& g, const std::string& ddv, const s
   HIP_CHECK(hipMemcpy(hv, d_dt_, sizeof(hv), hipMemcpyDeviceToHost));
   std::vector<int> planes(p.nkx_loc);
   for (int i = 0; i < p.nkx_loc; ++i) planes[i] = p.kx_fft_pos(p.kx0 + i);
-  auto pack = [&](const std::vector<std::complex<double>>& f) {
-    std::vector<double> d(static_cast<size_t>(p.nkx_loc) * NZ * N * 2, 0.0);
+  // pencil ranks own a kz range of each plane: read-modify-write (ranks take turns below)
+  auto pack = [&](const std::vector<std::complex<double>>& f, std::vector<double>& d) {
     for (int i = 0; i < p.nkx_loc; ++i)
-      for (int kz = 0; kz < p.nkz; ++kz)
+      for (int kzl = 0; kzl < p.nkz_loc; ++kzl)
         for (int j = 0; j < N; ++j) {
-          const auto v = f[static_cast<size_t>(j) * lines + i * p.nkz + kz] * N2;
-          const size_t o = ((static_cast<size_t>(i) * NZ + kz) * N + j) * 2;
+          const auto v = f[static_cast<size_t>(j) * lines + i * p.nkz_loc + kzl] * N2;
+          const size_t o = ((static_cast<size_t>(i) * NZ + p.kz0 + kzl) * N + j) * 2;
           d[o] = v.real();
           d[o + 1] = v.imag();
         }
-    return d;
   };
   std::map<std::string, double> attrs = {{"time", hv[1]}, {"dt", hv[0]}, {"step", static_cast<double>(nstep_)},
                                          {"Re", cfg_.Re},  {"Q", cfg_.Q},   {"LX", cfg_.LX},
@@ -784,14 +845,21 @@ void Solver::write_restart(const std::string& g, const std::string& ddv, const s
   for (int which = 0; which < 2; ++which) {
     const std::string& path = which == 0 ? g : ddv;
     if (path.empty() || path == "-") continue;
-    auto data = pack(which == 0 ? om : phi);
     if (p.rank == 0) {
       h5_create_field(path, p.NX, N, NZ, false);
       h5_write_attrs(path, attrs);
     }
     for (int r = 0; r < p.P; ++r) {
       barrier();
-      if (r == p.rank) h5_write_planes(path, planes, data);
+      if (r == p.rank) {
+        std::vector<double> data(static_cast<size_t>(p.nkx_loc) * NZ * N * 2, 0.0);
+        if (p.pencil()) {
+          int dims[3];
+          h5_read_planes(path, planes, data, dims);
+        }
+        pack(which == 0 ? om : phi, data);
+        h5_write_planes(path, planes, data);
+      }
     }
     barrier();
   }
@@ -817,10 +885,10 @@ void Solver::read_restart(const std::string& g, const std::string& ddv, const st
     CH_CHECK(dims[0] == p.NX && dims[1] == N && dims[2] == 2 * NZ,
              "restart file " << path << " has dims " << dims[0] << "x" << dims[1] << "x" << dims[2]);
     for (int i = 0; i < p.nkx_loc; ++i)
-      for (int kz = 0; kz < p.nkz; ++kz)
+      for (int kzl = 0; kzl < p.nkz_loc; ++kzl)
         for (int j = 0; j < N; ++j) {
-          const size_t o = ((static_cast<size_t>(i) * NZ + kz) * N + j) * 2;
-          f[static_cast<size_t>(j) * lines + i * p.nkz + kz] = std::complex<double>(d[o], d[o + 1]) / N2;
+          const size_t o = ((static_cast<size_t>(i) * NZ + p.kz0 + kzl) * N + j) * 2;
+          f[static_cast<size_t>(j) * lines + i * p.nkz_loc + kzl] = std::complex<double>(d[o], d[o + 1]) / N2;
         }
   };
   unpack(g, om);

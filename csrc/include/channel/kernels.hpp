@@ -41,7 +41,8 @@ struct SpecArgs {
   // geometry
   int N = 0;              // NY
   int lines = 0;          // local lines = nkx_loc * nkz, line = ikx_local * nkz + kz
-  int nkz = 0, kx0 = 0, nkx = 0, Kx = 0;
+  int nkz = 0, kx0 = 0, nkx = 0, Kx = 0;   // nkz = local kz count (pencil: a kz range)
+  int kz0 = 0;            // first local kz (pencil)
   double ax = 1, az = 2;  // 2 pi / LX, 2 pi / LZ
   double nu = 1.0 / 3250.0;
   // RK3 substep (mode 1)
@@ -93,10 +94,15 @@ struct XDst {             // destination blocks for the forward x-transform (per
 };
 
 struct XArgs {
-  int NX = 0, nkx = 0, Kx = 0, nkz = 0, ny = 0;   // ny = local y planes
+  int NX = 0, nkx = 0, Kx = 0, nkz = 0, ny = 0;   // ny = local y planes, nkz = local kz count
   int nfields = 1;
   long long field_stride_spec = 0;   // element stride between fields in the spectral buffers
   long long field_stride_phys = 0;   // element stride between fields in the physical buffers
+  // x-expanded buffer blocked by x range (pencil B exchange): x in [x_start[d], x_start[d+1]) lives
+  // at poff[d] + (y * nx_d + x - x_start[d]) * nkz.  One segment = plain [y][x][kz].
+  int npseg = 1;
+  int x_start[9] = {0};
+  long long poff[8] = {0};
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
@@ -104,7 +110,12 @@ void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& 
 void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s);
 
 struct ZArgs {
-  int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;
+  int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;   // NX = local x count (rows = ny * NX)
+  // rows blocked by kz range (pencil B exchange): kz in [kz_start[s], kz_start[s+1]) of row r lives
+  // at off[s] + r * nkz_s + kz - kz_start[s].  One segment = plain [row][kz].
+  int nseg = 1;
+  int kz_start[9] = {0};
+  long long off[8] = {0};
   long long field_stride = 0;        // element stride between the 6 input fields
   double scale = 1.0;                // forward normalisation 1/(NX*Nzp)
   const double* inv_dy = nullptr;    // [NY] 1/local spacing for the CFL estimate

@@ -101,8 +101,8 @@ class Solver {
   void free_all();
   void transforms(int substep, bool stats);
   void kspec(int mode, int substep, bool stats);
-  void a2a_backward(int f);
-  void a2a_forward(int f);
+  void a2a_spec(const void* spec, void* xb, bool to_phys);
+  void a2a_rows(void* xexp, void* zrows, bool to_z);
   void step_body(bool stats);
   void ev(int phase, bool end);
   void write_logs(const StepLog& L, bool verbose);
@@ -122,8 +122,9 @@ class Solver {
   void* state_ = nullptr;  // phi, omega, Rphi, Romega (4 * spec)
   void* out_ = nullptr;    // 6 * spec
   void* phys_ = nullptr;   // 6 * phys
-  void* xbuf_ = nullptr;   // P>1: 6 * ny_loc*nkx*nkz
-  size_t spec_ = 0, physn_ = 0, xstride_ = 0;
+  void* xbuf_ = nullptr;   // P>1: 6 * ny_loc*nkx*nkz_loc (A-exchange blocks)
+  void* zbuf_ = nullptr;   // pencil: 6 * ny_loc*nx_loc*nkz (B-exchange blocks, z stage in place)
+  size_t spec_ = 0, physn_ = 0, xstride_ = 0, zstride_ = 0;
 
   // device scalars / diagnostics (one allocation)
   void* dscal_ = nullptr;
@@ -138,7 +139,7 @@ class Solver {
   bool kprof_on_ = false;
   double* d_invdy_ = nullptr;
 
-  std::vector<hipEvent_t> ev_a2a_, ev_xf_;
+  std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
   std::vector<hipEvent_t> ph_ev_;
   std::vector<double> ph_ms_;

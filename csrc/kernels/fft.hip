@@ -76,7 +76,7 @@ __device__ __forceinline__ int find_block(const int* start, int n, int i) {
 // into registers right after the current tile is staged into LDS, so they are in flight during
 // the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
-template <int NX, typename T>
+template <int NX, typename T, bool SEG>
 __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
                                                             const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -143,12 +143,20 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
     for (int e = tid; e < NX * C; e += NT) {
       const int x = e / C, c = e - x * C;
       const int kz = kz0 + c;
-      if (kz < a.nkz) out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+      if (kz < a.nkz) {
+        if constexpr (SEG) {
+          const int d = find_block(a.x_start, a.npseg, x);
+          const int nxd = a.x_start[d + 1] - a.x_start[d];
+          out[a.poff[d] + (static_cast<long long>(y) * nxd + (x - a.x_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        } else {
+          out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        }
+      }
     }
   }
 }
 
-template <int NX, typename T>
+template <int NX, typename T, bool SEG>
 __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
                                                            const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -173,7 +181,16 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
       const int x = e / C, c = e - x * C;
       const int kz = kz0 + c;
       v[q] = T2{0, 0};
-      if (e < NX * C && kz < a.nkz) v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      if (e < NX * C && kz < a.nkz) {
+        if constexpr (SEG) {
+          const int d = find_block(a.x_start, a.npseg, x);
+          const int nxd = a.x_start[d + 1] - a.x_start[d];
+          v[q] = in[static_cast<unsigned>(a.poff[d]) +
+                    static_cast<unsigned>(y * nxd + x - a.x_start[d]) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+        } else {
+          v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+        }
+      }
     }
   };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
@@ -232,7 +249,7 @@ static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddle
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
     } else {
       constexpr int C = XCfg<NN, T>::C;
-      auto kern = xfft_backward_kernel<NN, T>;
+      auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true> : xfft_backward_kernel<NN, T, false>;
       const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
       dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
       hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, src, static_cast<T2*>(phys),
@@ -250,7 +267,7 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
     } else {
       constexpr int C = XCfg<NN, T>::C;
-      auto kern = xfft_forward_kernel<NN, T>;
+      auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true> : xfft_forward_kernel<NN, T, false>;
       const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
       dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
       hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, static_cast<const T2*>(phys), dst,
@@ -260,7 +277,21 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
   HIP_LAUNCH_CHECK(s);
 }
 
-void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s) {
+// one segment: plain [y][x][kz]; otherwise the table must tile [0, NX)
+static XArgs norm_pseg(const XArgs& in) {
+  XArgs a = in;
+  if (a.npseg <= 1) {
+    a.npseg = 1;
+    a.x_start[0] = 0;
+    a.x_start[1] = a.NX;
+    a.poff[0] = 0;
+  }
+  CH_CHECK(a.npseg <= 8 && a.x_start[0] == 0 && a.x_start[a.npseg] == a.NX, "x transform: bad x segment table");
+  return a;
+}
+
+void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s) {
+  const XArgs a = norm_pseg(a_in);
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_backward: twiddle table mismatch");
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
   CH_CHECK(a.nkx <= 2 * (a.NX / 3) + 1, "xfft_backward: more retained kx than the 2/3 rule allows");
@@ -269,7 +300,8 @@ void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& 
   else xb_launch<float>(a, src, phys, tw, s);
 }
 
-void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s) {
+void xfft_forward(const XArgs& a_in, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s) {
+  const XArgs a = norm_pseg(a_in);
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_forward: twiddle table mismatch");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_forward: per-field plane block exceeds 32-bit offsets");
   if (fp64) xf_launch<double>(a, phys, dst, tw, s);
@@ -286,7 +318,7 @@ __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
 // physical fields stay in registers (each lane owns points n = lane + 64 i of the row).
 constexpr int ZW = 4;
 
-template <int NZP, typename T>
+template <int NZP, typename T, bool SEG>
 __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                     const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -304,6 +336,15 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   const int Kz = a.nkz - 1, nkz = a.nkz;
   const long long fs = a.field_stride;
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
+  // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz)
+  auto zaddr = [&](int k) -> long long {
+    if constexpr (SEG) {
+      const int sb = find_block(a.kz_start, a.nseg, k);
+      return a.off[sb] + r * (a.kz_start[sb + 1] - a.kz_start[sb]) + (k - a.kz_start[sb]);
+    } else {
+      return r * nkz + k;
+    }
+  };
 
   if (r < nrows) {  // wave-uniform
     T2 ph[3][EP];
@@ -311,15 +352,16 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     for (int p = 0; p < 3; ++p) {
       // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
       // (a real z-row has a real mean), zero padding between Kz and N-Kz.
-      const T2* A = fields + (2 * p) * fs + r * nkz;
-      const T2* B = fields + (2 * p + 1) * fs + r * nkz;
+      const T2* A = fields + (2 * p) * fs;
+      const T2* B = fields + (2 * p + 1) * fs;
       constexpr int MK = (NZP / 2 + 63) / 64;
       T2 va[MK], vb[MK];
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
         const int k = lane + 64 * i;
-        va[i] = k < nkz ? A[k] : T2{0, 0};
-        vb[i] = k < nkz ? B[k] : T2{0, 0};
+        const long long o = k < nkz ? zaddr(k) : 0;
+        va[i] = k < nkz ? A[o] : T2{0, 0};
+        vb[i] = k < nkz ? B[o] : T2{0, 0};
       }
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
@@ -366,8 +408,9 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     for (int k = lane; k < nkz; k += 64) {
       const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
-      fields[0 * fs + r * nkz + k] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
-      fields[1 * fs + r * nkz + k] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+      const long long o = zaddr(k);
+      fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+      fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -379,7 +422,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
     for (int k = lane; k < nkz; k += 64) {
       const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
-      fields[2 * fs + r * nkz + k] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+      fields[2 * fs + zaddr(k)] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
     }
   }
   // block maxima -> one atomicMax per block and quantity
@@ -412,14 +455,26 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
     } else {
       const long long nrows = static_cast<long long>(a.ny) * a.NX;
       dim3 grid(static_cast<unsigned>((nrows + ZW - 1) / ZW));
-      hipLaunchKernelGGL((zphys_kernel<NN, T>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
-                         static_cast<const T2*>(tw.buf));
+      if (a.nseg > 1)
+        hipLaunchKernelGGL((zphys_kernel<NN, T, true>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
+                           static_cast<const T2*>(tw.buf));
+      else
+        hipLaunchKernelGGL((zphys_kernel<NN, T, false>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
+                           static_cast<const T2*>(tw.buf));
     }
   });
   HIP_LAUNCH_CHECK(s);
 }
 
-void zphys(const ZArgs& a, void* fields, const Twiddles& tw, bool fp64, hipStream_t s) {
+void zphys(const ZArgs& a_in, void* fields, const Twiddles& tw, bool fp64, hipStream_t s) {
+  ZArgs a = a_in;
+  if (a.nseg <= 1) {
+    a.nseg = 1;
+    a.kz_start[0] = 0;
+    a.kz_start[1] = a.nkz;
+    a.off[0] = 0;
+  }
+  CH_CHECK(a.nseg <= 8 && a.kz_start[0] == 0 && a.kz_start[a.nseg] == a.nkz, "zphys: bad kz segment table");
   CH_CHECK(tw.n == a.Nzp && tw.fp64 == fp64, "zphys: twiddle table mismatch");
   CH_CHECK(a.nkz - 1 < a.Nzp / 2, "zphys: retained kz must be below Nyquist");
   if (a.ny == 0) return;

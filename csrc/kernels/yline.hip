@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const bool has_next = a.mode == 1 && next_line0 < a.lines;
 
   const int ikx = valid ? line / a.nkz : 0;
-  const int kz = valid ? line - ikx * a.nkz : 0;
+  const int kz = valid ? a.kz0 + (line - ikx * a.nkz) : 0;
   const int ig = a.kx0 + ikx;
   const int kx = ig <= a.Kx ? ig : ig - a.nkx;
   const double al = a.ax * kx, be = a.az * kz;

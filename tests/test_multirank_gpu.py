@@ -1,4 +1,4 @@
-"""Slab-decomposed GPU solver with P ranks sharing the one GPU of the test box.
+"""Slab- and pencil-decomposed GPU solver with P ranks sharing the one GPU of the test box.
 
 RCCL refuses two ranks on one device, so these runs use the host shared-memory communicator
 (ShmComm, "shm:" unique id), which drives exactly the same send/recv block addressing, x-transform
@@ -27,7 +27,7 @@ def _global_state():
     return phi, om, 0.75 * 1.8 * (1 - ops.y ** 2)
 
 
-def _worker(rank, world, shm, outdir, nsteps):
+def _worker(rank, world, shm, outdir, nsteps, pr=1):
     import torch  # noqa: F401
 
     from channel_gpu_amd import require_native
@@ -35,24 +35,37 @@ def _worker(rank, world, shm, outdir, nsteps):
 
     C = require_native()
     cfg = default_config(**GRID, Re=400.0, precision="fp64", dt_fixed=0.01, ic="zero", stats_every=0,
-                         log_every=0, symmetry_every=0)
+                         log_every=0, symmetry_every=0, decomposition="pencil" if pr > 1 else "slab", pr=pr)
     s = C.Solver(cfg, rank, world, 0, shm.encode())
     p = s.plan
+    assert p.Pr == pr and p.Pr * p.Pc == world
     phi, om, U = _global_state()
     sl = slice(p.kx0, p.kx0 + p.nkx_loc)
-    s.set_state(np.ascontiguousarray(phi[:, sl]), np.ascontiguousarray(om[:, sl]), U)
+    sz = slice(p.kz0, p.kz0 + p.nkz_loc)
+    s.set_state(np.ascontiguousarray(phi[:, sl, sz]), np.ascontiguousarray(om[:, sl, sz]), U)
     s.prepare()
     for _ in range(nsteps):
         s.step(False)
     gphi, gom, gU = s.get_state()
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), phi=gphi, om=gom, U=gU, health=s.health())
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), phi=gphi, om=gom, U=gU, health=s.health(), kx0=p.kx0,
+             kz0=p.kz0)
     if C.hdf5_available():
         s.write_restart(os.path.join(outdir, "G.h5"), os.path.join(outdir, "DDV.h5"), os.path.join(outdir, "U.bin"))
     del s
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multirank_matches_oracle(native, world):
+def _assemble(parts, field):
+    nkx = sum(q[field].shape[1] for q in parts if int(q["kz0"]) == 0)
+    nkz = sum(q[field].shape[2] for q in parts if int(q["kx0"]) == 0)
+    out = np.zeros((parts[0][field].shape[0], nkx, nkz), complex)
+    for q in parts:
+        a, b = int(q["kx0"]), int(q["kz0"])
+        out[:, a:a + q[field].shape[1], b:b + q[field].shape[2]] = q[field]
+    return out
+
+
+@pytest.mark.parametrize("world,pr", [(2, 1), (3, 1), (2, 2), (4, 2)])
+def test_multirank_matches_oracle(native, world, pr):
     nsteps = 2
     ref = ora.OracleSolver(**GRID, Re=400.0, dt_fixed=0.01)
     phi, om, U = _global_state()
@@ -61,10 +74,11 @@ def test_multirank_matches_oracle(native, world):
         ref.step()
     shm = f"shm:chtest_{uuid.uuid4().hex[:12]}"
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, shm, d, nsteps), nprocs=world, join=True, start_method="spawn")
-        parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
-        gphi = np.concatenate([q["phi"] for q in parts], axis=1)
-        gom = np.concatenate([q["om"] for q in parts], axis=1)
+        mp.start_processes(_worker, args=(world, shm, d, nsteps, pr), nprocs=world, join=True,
+                           start_method="spawn")
+        parts = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
+        gphi = _assemble(parts, "phi")
+        gom = _assemble(parts, "om")
         assert all(int(q["health"]) == 0 for q in parts)
         assert np.abs(gphi - ref.phi).max() < 1e-9 * np.abs(ref.phi).max()
         assert np.abs(gom - ref.om).max() < 1e-9 * np.abs(ref.om).max()

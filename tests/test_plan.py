@@ -2,7 +2,8 @@
 (NX != NY, NY % P != 0, NY = 385 at P = 8)."""
 import pytest
 
-from channel_gpu_amd.parallel.decomposition import SlabDecomposition, balanced_split
+from channel_gpu_amd.parallel.decomposition import (PencilDecomposition, SlabDecomposition, auto_pencil_grid,
+                                                    balanced_split)
 
 
 def cfg(native, **kw):
@@ -61,3 +62,27 @@ def test_a2a_volume_model():
     # per rank and step: 27 transposes of 7/8 of its retained-field slab (0.72 GB / 8 per field)
     # ~= 2.1 GB; at ~7 x 153 GB/s of xGMI per GPU that is ~2 ms of ideal all-to-all per step
     assert 1.5e9 < b < 3.0e9
+
+
+@pytest.mark.parametrize("P,pr", [(4, 2), (8, 2), (8, 4), (6, 3), (8, 0)])
+def test_pencil_plan_matches_python(native, P, pr):
+    c = cfg(native, NX=1024, NY=385, NZ=513, decomposition="pencil", pr=pr)
+    Pr, Pc = (pr, P // pr) if pr else auto_pencil_grid(P)
+    d = PencilDecomposition(1024, 385, 513, Pr, Pc)
+    seen = set()
+    for r in range(P):
+        p = native.Plan.make(c, P, r)
+        assert (p.Pr, p.Pc) == (Pr, Pc) and p.pencil() == (Pr > 1)
+        L = d.local(r)
+        got = dict(kx0=p.kx0, nkx_loc=p.nkx_loc, y0=p.y0, ny_loc=p.ny_loc, kz0=p.kz0, nkz_loc=p.nkz_loc, x0=p.x0,
+                   nx_loc=p.nx_loc)
+        assert got == L
+        assert p.owns_mean() == (r == 0) if hasattr(p, "owns_mean") else True
+        seen.update((kx, kz) for kx in range(p.kx0, p.kx0 + p.nkx_loc) for kz in range(p.kz0, p.kz0 + p.nkz_loc))
+    assert len(seen) == 683 * 342   # every retained mode owned exactly once
+
+
+def test_pencil_grid_mismatch(native):
+    c = cfg(native, NX=64, NY=65, NZ=33, decomposition="pencil", pr=3)
+    with pytest.raises(RuntimeError):
+        native.Plan.make(c, 4, 0)
