@@ -205,7 +205,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       RW(NX) RW(NY) RW(NZ) RW(in_G) RW(in_DDV) RW(in_UMEAN) RW(out_G) RW(out_DDV) RW(out_UMEAN) RW(path) RW(Re) RW(Q)
       RW(LX) RW(LZ) RW(stretch) RW(nsteps) RW(t_end) RW(cfl) RW(dt_fixed) RW(dt_max) RW(cfl_mode) RW(stats_every)
       RW(symmetry_every) RW(checkpoint_every) RW(log_every) RW(precision) RW(decomposition) RW(pr) RW(pc) RW(seed)
-      RW(ic) RW(ic_amplitude) RW(forcing) RW(health_check);
+      RW(ic) RW(ic_amplitude) RW(forcing) RW(health_check) RW(health_every) RW(on_nan) RW(snapshot_every)
+      RW(max_rollbacks) RW(rollback_cfl_factor) RW(spectra_every) RW(spectra_planes) RW(log_json);
 #undef RW
 
   m.def("parse_config_tree", [](const std::string& text) { return ConfigTree::parse_string(text).items(); });
@@ -333,6 +334,34 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("write_restart", &Solver::write_restart, py::call_guard<py::gil_scoped_release>())
       .def("read_restart", &Solver::read_restart, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Solver::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("take_snapshot", &Solver::take_snapshot, py::call_guard<py::gil_scoped_release>())
+      .def("rollback", &Solver::rollback, py::call_guard<py::gil_scoped_release>())
+      .def("rollbacks", &Solver::rollbacks)
+      .def("snapshot_step", &Solver::snapshot_step)
+      .def("cfl", &Solver::cfl)
+      .def("inject_nan", &Solver::inject_nan, py::arg("field") = 0)
+      .def("spectra",
+           [](Solver& s) {
+             Solver::Spectra sp;
+             {
+               py::gil_scoped_release r;
+               sp = s.spectra();
+             }
+             const Plan& p = s.plan();
+             const int np = static_cast<int>(sp.planes.size());
+             auto arr = [](const std::vector<double>& v, std::vector<py::ssize_t> shape) {
+               py::array_t<double> a(shape);
+               std::copy(v.begin(), v.end(), a.mutable_data());
+               return a;
+             };
+             py::dict d;
+             d["planes"] = sp.planes;
+             d["ekx"] = arr(sp.ekx, {3, np, p.Kx + 1});
+             d["ekz"] = arr(sp.ekz, {3, np, p.nkz});
+             d["map"] = arr(sp.map, {3, p.nkx, p.nkz});
+             return d;
+           },
+           "energy spectra of u, v, w of the current state at cfg.spectra_planes (global)")
       .def("field", &field_tensor, "zero-copy torch view of a device field [NY, nkx_loc, nkz]")
       .def("phys", &phys_tensor, "zero-copy torch view of the physical-stage buffer [6, ny_loc, NX, nkz]");
 }

@@ -55,6 +55,13 @@ void RcclComm::abort() {
   comm_ = nullptr;
 }
 
+bool RcclComm::async_error() {
+  if (!comm_) return true;
+  ncclResult_t r = ncclSuccess;
+  if (ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &r) != ncclSuccess) return true;
+  return r != ncclSuccess && r != ncclInProgress;
+}
+
 void RcclComm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
                          void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
                          hipStream_t s) {
@@ -96,6 +103,7 @@ ShmComm::ShmComm(int rank, int nranks, const std::string& name) : name_("/" + na
   size_ = nranks;
   const char* mb = std::getenv("CHANNEL_SHM_SLOT_MB");
   slot_bytes_ = static_cast<size_t>(mb ? std::atoi(mb) : 16) << 20;
+  if (const char* t = std::getenv("CHANNEL_COMM_TIMEOUT_S")) timeout_s_ = std::atof(t);
   bytes_ = kHdr + static_cast<size_t>(nranks) * nranks * slot_bytes_;
   int fd = -1;
   if (rank == 0) {
@@ -136,7 +144,7 @@ ShmComm::ShmComm(int rank, int nranks, const std::string& name) : name_("/" + na
 
 ShmComm::~ShmComm() {
   try {
-    barrier();
+    if (!failed_) barrier();
   } catch (...) {
   }
   if (base_) munmap(base_, bytes_);
@@ -152,7 +160,10 @@ void ShmComm::barrier() {
   } else {
     const auto t0 = std::chrono::steady_clock::now();
     while (h->sense.load() != my_sense) {
-      CH_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(300), "ShmComm barrier timeout");
+      if (timeout_s_ > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_) {
+        failed_ = true;
+        CH_CHECK(false, "ShmComm barrier timeout after " << timeout_s_ << " s (a peer rank died or hung)");
+      }
       std::this_thread::yield();
     }
   }

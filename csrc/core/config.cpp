@@ -211,6 +211,14 @@ Config Config::from_tree(const ConfigTree& t) {
   c.ic_amplitude = t.get_double(pick(t, "ic_amplitude"), c.ic_amplitude);
   c.forcing = t.get_string(pick(t, "forcing"), c.forcing);
   c.health_check = t.get_bool(pick(t, "health_check"), c.health_check);
+  c.health_every = static_cast<int>(t.get_int(pick(t, "health_every"), c.health_every));
+  c.on_nan = t.get_string(pick(t, "on_nan"), c.on_nan);
+  c.snapshot_every = static_cast<int>(t.get_int(pick(t, "snapshot_every"), c.snapshot_every));
+  c.max_rollbacks = static_cast<int>(t.get_int(pick(t, "max_rollbacks"), c.max_rollbacks));
+  c.rollback_cfl_factor = t.get_double(pick(t, "rollback_cfl_factor"), c.rollback_cfl_factor);
+  c.spectra_every = static_cast<int>(t.get_int(pick(t, "spectra_every"), c.spectra_every));
+  c.spectra_planes = t.get_string(pick(t, "spectra_planes"), c.spectra_planes);
+  c.log_json = t.get_string(pick(t, "log_json"), c.log_json);
   // Reference semantics: input files given => start from file.
   if (c.in_G != "-" && c.in_DDV != "-" && !t.has(pick(t, "ic"))) c.ic = "file";
   c.validate();
@@ -229,6 +237,23 @@ Config Config::from_file(const std::string& path, const std::vector<std::string>
   return from_tree(t);
 }
 
+std::vector<int> Config::spectra_plane_list() const {
+  std::vector<int> out;
+  std::string tok;
+  std::istringstream is(spectra_planes);
+  while (std::getline(is, tok, ',')) {
+    tok.erase(0, tok.find_first_not_of(" \t"));
+    tok.erase(tok.find_last_not_of(" \t") + 1);
+    if (tok.empty()) continue;
+    char* end = nullptr;
+    const long v = std::strtol(tok.c_str(), &end, 10);
+    CH_CHECK(end && *end == '\0', "spectra_planes: '" << tok << "' is not an integer");
+    out.push_back(static_cast<int>(v));
+  }
+  if (out.empty()) out.push_back(NY / 2);
+  return out;
+}
+
 static bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 void Config::validate() const {
@@ -245,8 +270,14 @@ void Config::validate() const {
   CH_CHECK(forcing == "implicit" || forcing == "parity", "forcing must be implicit|parity");
   CH_CHECK(ic == "random" || ic == "laminar" || ic == "file" || ic == "os_mode" || ic == "zero",
            "ic must be random|laminar|file|os_mode|zero");
-  CH_CHECK(stats_every >= 0 && symmetry_every >= 0 && checkpoint_every >= 0 && log_every >= 0,
-           "cadences must be >= 0");
+  CH_CHECK(stats_every >= 0 && symmetry_every >= 0 && checkpoint_every >= 0 && log_every >= 0 &&
+               spectra_every >= 0 && snapshot_every >= 0 && health_every >= 1,
+           "cadences must be >= 0 (health_every >= 1)");
+  CH_CHECK(on_nan == "abort" || on_nan == "rollback", "on_nan must be abort|rollback");
+  CH_CHECK(rollback_cfl_factor > 0 && rollback_cfl_factor <= 1, "rollback_cfl_factor must be in (0, 1]");
+  CH_CHECK(max_rollbacks >= 0, "max_rollbacks must be >= 0");
+  for (int j : spectra_plane_list())
+    CH_CHECK(j >= 0 && j < NY, "spectra_planes: y index " << j << " outside [0, NY)");
 }
 
 std::string Config::to_string() const {
@@ -267,6 +298,10 @@ std::string Config::to_string() const {
   o << "  pr = " << pr << ";\n  pc = " << pc << ";\n  seed = " << seed << ";\n";
   o << "  ic = \"" << ic << "\";\n  ic_amplitude = " << ic_amplitude << ";\n";
   o << "  forcing = \"" << forcing << "\";\n  health_check = " << (health_check ? "true" : "false") << ";\n";
+  o << "  health_every = " << health_every << ";\n  on_nan = \"" << on_nan << "\";\n";
+  o << "  snapshot_every = " << snapshot_every << ";\n  max_rollbacks = " << max_rollbacks << ";\n";
+  o << "  rollback_cfl_factor = " << rollback_cfl_factor << ";\n  spectra_every = " << spectra_every << ";\n";
+  o << "  spectra_planes = \"" << spectra_planes << "\";\n  log_json = \"" << log_json << "\";\n";
   o << "};\n";
   return o.str();
 }

@@ -8,7 +8,10 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <chrono>
 #include <mutex>
+#include <sstream>
+#include <thread>
 
 #include "channel/common.hpp"
 #include "channel/io.hpp"
@@ -87,6 +90,7 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
     // grid sizes); capturing RCCL into the step graph is opt-in (CHANNEL_GRAPH_MULTI=1).
     const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
     if (!comm_->graph_capturable() || !(gm && std::atoi(gm) == 1)) use_graph_ = false;
+    if (const char* t = std::getenv("CHANNEL_COMM_TIMEOUT_S")) comm_timeout_s_ = std::atof(t);
   }
   ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
   tw_x_.build(plan_.NX, fp64_);
@@ -173,9 +177,9 @@ void Solver::free_all() {
   for (auto e : ph_ev_) (void)hipEventDestroy(e);
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
     if (e) (void)hipEventDestroy(e);
-  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_})
+  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_})
     if (p) (void)hipFree(p);
-  state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = nullptr;
+  state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = nullptr;
 }
 
 void* Solver::field_ptr(int f) const {
@@ -630,16 +634,42 @@ void Solver::substep_debug(int n) {
 
 void Solver::transforms_debug(bool dt_upd) { transforms(dt_upd ? 0 : 1, false); }
 
+// P > 1: poll instead of blocking so that a dead or hung peer (RCCL async error, or no progress
+// for CHANNEL_COMM_TIMEOUT_S seconds) aborts the communicator and raises on every surviving rank
+// instead of hanging the job (the reference's exit(1) left peers blocked in MPI, check.cu:67-79).
+void Solver::wait(hipStream_t s) {
+  if (!comm_) {
+    HIP_CHECK(hipStreamSynchronize(s));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int it = 0;; ++it) {
+    const hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    if (comm_->async_error()) {
+      comm_->abort();
+      CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (comm_timeout_s_ > 0 && el > comm_timeout_s_) {
+      comm_->abort();
+      CH_CHECK(false, "rank " << plan_.rank << ": no progress for " << comm_timeout_s_ << " s; communicator aborted");
+    }
+    if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 void Solver::synchronize() {
-  HIP_CHECK(hipStreamSynchronize(s_comp_));
-  HIP_CHECK(hipStreamSynchronize(s_comm_));
+  wait(s_comp_);
+  wait(s_comm_);
 }
 
 void Solver::barrier() {
   if (comm_) {
     // tiny allreduce as a device barrier, then host sync
     comm_->allreduce_max_u32(d_health_, 1, s_comm_);
-    HIP_CHECK(hipStreamSynchronize(s_comm_));
+    wait(s_comm_);
   }
   synchronize();
 }
@@ -678,7 +708,7 @@ StepLog Solver::log() {
 unsigned Solver::health() {
   if (comm_) {
     comm_->allreduce_max_u32(d_health_, 1, s_comm_);
-    HIP_CHECK(hipStreamSynchronize(s_comm_));
+    wait(s_comm_);
   }
   unsigned h = 0;
   HIP_CHECK(hipMemcpy(&h, d_health_, sizeof(h), hipMemcpyDeviceToHost));
@@ -782,8 +812,14 @@ void Solver::write_stats_files(const std::vector<double>& st) {
 void Solver::run(long nsteps, bool verbose) {
   if (!prepared_) prepare();
   const int se = cfg_.stats_every, le = cfg_.log_every, ce = cfg_.checkpoint_every, ye = cfg_.symmetry_every;
+  const int he = cfg_.health_every, pe = cfg_.spectra_every;
+  const bool rb = cfg_.on_nan == "rollback";
+  const int sn = cfg_.snapshot_every > 0 ? cfg_.snapshot_every : he;
   if (stats_pending_ && se > 0 && nstep_ % se == 0) write_stats_files(stats());
   stats_pending_ = false;
+  if (rb && snap_step_ < 0) take_snapshot();
+  auto t_log = std::chrono::steady_clock::now();
+  long s_log = nstep_;
   for (long s = 0; s < nsteps; ++s) {
     const bool want_stats = se > 0 && (nstep_ + 1) % se == 0;
     step(want_stats);
@@ -792,16 +828,34 @@ void Solver::run(long nsteps, bool verbose) {
       stats_pending_ = false;
     }
     const bool do_log = le > 0 && nstep_ % le == 0;
-    if (do_log || (cfg_.health_check && nstep_ % 100 == 0)) {
+    if (do_log || (cfg_.health_check && nstep_ % he == 0)) {
       StepLog L = log();
       if (L.health) {
+        if (rb && rollbacks_ < cfg_.max_rollbacks && snap_step_ >= 0) {
+          const long lost = nstep_ - snap_step_;
+          if (plan_.rank == 0)
+            std::fprintf(stderr, "[channel] non-finite state at step %ld; rolling back to step %ld, cfl %g -> %g\n",
+                         L.step, snap_step_, cfg_.cfl, cfg_.cfl * cfg_.rollback_cfl_factor);
+          rollback();
+          s = std::max(-1L, s - lost);  // the lost steps are redone
+          continue;
+        }
         std::fprintf(stderr, "[channel] non-finite state detected at step %ld (t=%g, dt=%g); aborting\n", L.step,
                      L.time, L.dt);
         if (comm_) comm_->abort();
         CH_CHECK(false, "health check failed at step " << L.step);
       }
-      if (do_log) write_logs(L, verbose);
+      if (rb && nstep_ - snap_step_ >= sn) take_snapshot();
+      if (do_log) {
+        const auto t = std::chrono::steady_clock::now();
+        const double ms = 1e3 * std::chrono::duration<double>(t - t_log).count() / std::max(1L, nstep_ - s_log);
+        t_log = t;
+        s_log = nstep_;
+        write_logs(L, verbose);
+        write_json(L, ms);
+      }
     }
+    if (pe > 0 && nstep_ % pe == 0) write_spectra_files(spectra());
     if (ye > 0 && nstep_ % ye == 0 && !comm_) {
       symmetrize();
       prepare();
@@ -813,6 +867,162 @@ void Solver::run(long nsteps, bool verbose) {
     if (cfg_.t_end > 0 && time() >= cfg_.t_end) break;
   }
   synchronize();
+}
+
+// ---- failure handling ------------------------------------------------------------------------------
+void Solver::invalidate_graphs() {
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  for (int i = 0; i < 2; ++i) {
+    if (gexec_[i]) (void)hipGraphExecDestroy(gexec_[i]);
+    gexec_[i] = nullptr;
+    graph_ok_[i] = false;
+  }
+}
+
+void Solver::take_snapshot() {
+  const size_t fb = spec_ * esz_;
+  if (!snap_) HIP_CHECK(hipMalloc(&snap_, 2 * fb + 2 * sizeof(double)));
+  char* d = static_cast<char*>(snap_);
+  HIP_CHECK(hipMemcpyAsync(d, field_ptr(PHI), 2 * fb, hipMemcpyDeviceToDevice, s_comp_));  // PHI, OMEGA adjacent
+  HIP_CHECK(hipMemcpyAsync(d + 2 * fb, d_dt_, 2 * sizeof(double), hipMemcpyDeviceToDevice, s_comp_));
+  snap_step_ = nstep_;
+}
+
+void Solver::rollback() {
+  CH_CHECK(snap_ && snap_step_ >= 0, "rollback: no snapshot");
+  synchronize();
+  const size_t fb = spec_ * esz_;
+  char* d = static_cast<char*>(snap_);
+  HIP_CHECK(hipMemcpyAsync(field_ptr(PHI), d, 2 * fb, hipMemcpyDeviceToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(d_dt_, d + 2 * fb, 2 * sizeof(double), hipMemcpyDeviceToDevice, s_comp_));
+  HIP_CHECK(hipMemsetAsync(field_ptr(RPHI), 0, 2 * fb, s_comp_));  // zeta_0 = 0: R is not needed at substep 0
+  HIP_CHECK(hipMemsetAsync(d_max_, 0, 4 * sizeof(float), s_comp_));
+  HIP_CHECK(hipMemsetAsync(d_health_, 0, sizeof(unsigned), s_comp_));
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+  nstep_ = snap_step_;
+  ++rollbacks_;
+  cfg_.cfl *= cfg_.rollback_cfl_factor;  // captured as a kernel argument: re-capture the graphs
+  invalidate_graphs();
+  prepared_ = false;
+  prepare();
+}
+
+void Solver::inject_nan(int f) {
+  // an interior point of line 1 of the field (line 0 on the owner rank holds U)
+  const size_t elem = static_cast<size_t>(plan_.NY / 2) * plan_.lines_loc() + std::min(1, plan_.lines_loc() - 1);
+  ::channel::inject_nan(field_ptr(f), elem, fp64_, s_comp_);
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
+}
+
+// ---- spectra --------------------------------------------------------------------------------------
+Solver::Spectra Solver::spectra() {
+  const Plan& p = plan_;
+  Spectra out;
+  out.planes = cfg_.spectra_plane_list();
+  const int np = static_cast<int>(out.planes.size());
+  const size_t nx = 3 * np * (p.Kx + 1), nz = 3 * np * p.nkz, nm = 3 * static_cast<size_t>(p.nkx) * p.nkz;
+  const size_t need = (nx + nz + nm) * sizeof(double) + np * sizeof(int);
+  if (spec_n_ < need) {
+    if (d_spec_) HIP_CHECK(hipFree(d_spec_));
+    HIP_CHECK(hipMalloc(&d_spec_, need));
+    spec_n_ = need;
+  }
+  double* ekx = static_cast<double*>(d_spec_);
+  double* ekz = ekx + nx;
+  double* map = ekz + nz;
+  int* planes = reinterpret_cast<int*>(map + nm);
+  HIP_CHECK(hipMemsetAsync(d_spec_, 0, (nx + nz + nm) * sizeof(double), s_comp_));
+  HIP_CHECK(hipMemcpyAsync(planes, out.planes.data(), np * sizeof(int), hipMemcpyHostToDevice, s_comp_));
+  SpectraArgs a;
+  a.u = field_ptr(OUT0);
+  a.v = field_ptr(OUT1);
+  a.w = field_ptr(OUT2);
+  a.lines = p.lines_loc();
+  a.nkx_loc = p.nkx_loc;
+  a.kx0 = p.kx0;
+  a.nkz_loc = p.nkz_loc;
+  a.kz0 = p.kz0;
+  a.nkx = p.nkx;
+  a.Kx = p.Kx;
+  a.nkz = p.nkz;
+  a.planes = planes;
+  a.nplanes = np;
+  a.ekx = ekx;
+  a.ekz = ekz;
+  a.map = map;
+  spectra_accumulate(a, fp64_, s_comp_);
+  if (comm_) {
+    HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_stats_, 0));
+    comm_->allreduce_sum_f64(ekx, nx + nz + nm, s_comm_);
+    wait(s_comm_);
+  }
+  synchronize();
+  out.ekx.resize(nx);
+  out.ekz.resize(nz);
+  out.map.resize(nm);
+  HIP_CHECK(hipMemcpy(out.ekx.data(), ekx, nx * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(out.ekz.data(), ekz, nz * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(out.map.data(), map, nm * sizeof(double), hipMemcpyDeviceToHost));
+  return out;
+}
+
+void Solver::write_spectra_files(const Spectra& sp) {
+  if (plan_.rank != 0) return;
+  const Plan& p = plan_;
+  const int np = static_cast<int>(sp.planes.size());
+  const double N2 = static_cast<double>(p.NX) * p.Nzp;
+  // reference layout (statistics.cu:272-320): NX rows (FFT-order kx) x NZ columns of |q|^2 in the
+  // file units (N2 * coefficient), plane planes[0]; overwritten each time like the reference's "w"
+  const char* maps[3] = {"Uspec.dat", "Vspec.dat", "Wspec.dat"};
+  for (int q = 0; q < 3; ++q) {
+    std::ofstream f(cfg_.path + maps[q]);
+    std::vector<int> ig_of_pos(p.NX, -1);
+    for (int i = 0; i < p.nkx; ++i) ig_of_pos[p.kx_fft_pos(i)] = i;
+    for (int x = 0; x < p.NX; ++x) {
+      for (int kz = 0; kz < p.NZ; ++kz) {
+        double v = 0.0;
+        if (ig_of_pos[x] >= 0 && kz < p.nkz) v = sp.map[(static_cast<size_t>(q) * p.nkx + ig_of_pos[x]) * p.nkz + kz];
+        f << " " << std::fixed << v * N2 * N2;
+      }
+      f << " \n";
+    }
+  }
+  // time series of 1-D spectra (true-coefficient units): one line per (plane, component)
+  auto app = [&](const char* name) { return std::ofstream(cfg_.path + name, std::ios::app); };
+  auto fx = app("SPECTRA_KX.dat");
+  auto fz = app("SPECTRA_KZ.dat");
+  double hv[2];
+  HIP_CHECK(hipMemcpy(hv, d_dt_, sizeof(hv), hipMemcpyDeviceToHost));
+  for (int pl = 0; pl < np; ++pl)
+    for (int q = 0; q < 3; ++q) {
+      fx << nstep_ << " " << std::scientific << hv[1] << " " << sp.planes[pl] << " " << "uvw"[q];
+      for (int k = 0; k <= p.Kx; ++k) fx << " " << sp.ekx[(static_cast<size_t>(q) * np + pl) * (p.Kx + 1) + k];
+      fx << "\n";
+      fz << nstep_ << " " << std::scientific << hv[1] << " " << sp.planes[pl] << " " << "uvw"[q];
+      for (int k = 0; k < p.nkz; ++k) fz << " " << sp.ekz[(static_cast<size_t>(q) * np + pl) * p.nkz + k];
+      fz << "\n";
+    }
+}
+
+void Solver::write_json(const StepLog& L, double ms_per_step) {
+  if (plan_.rank != 0 || cfg_.log_json.empty()) return;
+  std::ofstream f(cfg_.log_json, std::ios::app);
+  const double nu = 1.0 / cfg_.Re;
+  std::ostringstream o;
+  o.precision(9);
+  o << "{\"step\": " << L.step << ", \"time\": " << L.time << ", \"dt\": " << L.dt << ", \"cfl\": " << L.cflsum * L.dt
+    << ", \"umax\": " << L.umax << ", \"vmax\": " << L.vmax << ", \"wmax\": " << L.wmax << ", \"utau\": " << L.utau
+    << ", \"Re_tau\": " << L.utau / nu << ", \"flux\": " << L.flux << ", \"dpdx\": " << L.dpdx
+    << ", \"health\": " << L.health << ", \"rollbacks\": " << rollbacks_ << ", \"ms_per_step\": " << ms_per_step
+    << ", \"ranks\": " << plan_.P << ", \"grid\": [" << plan_.NX << ", " << plan_.NY << ", " << plan_.Nzp << "]";
+  if (phase_timing_) {
+    o << ", \"phase_ms\": [";
+    for (size_t i = 0; i < 4; ++i) o << (i ? ", " : "") << ph_ms_[i];
+    o << "]";
+  }
+  o << "}\n";
+  f << o.str();
 }
 
 // ---- restart I/O (Appendix B) --------------------------------------------------------------------

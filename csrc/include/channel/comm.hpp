@@ -35,6 +35,8 @@ class Comm {
   virtual void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) = 0;
   virtual void abort() = 0;
+  // asynchronous communicator failure (peer died, network error); polled by the solver's watchdog
+  virtual bool async_error() { return false; }
 
   static std::string new_unique_id();  // 128 raw bytes (RCCL)
   // "shm:<name>" -> ShmComm, otherwise an RCCL unique id
@@ -55,6 +57,7 @@ class RcclComm final : public Comm {
   void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
   void abort() override;
+  bool async_error() override;
 
  private:
   void* comm_ = nullptr;  // ncclComm_t
@@ -70,10 +73,13 @@ class ShmComm final : public Comm {
   void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
   void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
-  void abort() override {}
+  void abort() override { failed_ = true; }
+  bool async_error() override { return failed_; }
 
  private:
   void barrier();
+  bool failed_ = false;
+  double timeout_s_ = 300.0;  // CHANNEL_COMM_TIMEOUT_S
   char* slot(int src, int dst);
   template <typename T, typename Op>
   void allreduce(T* buf, size_t n, hipStream_t s, Op op);

@@ -68,6 +68,16 @@ struct Config {
   double ic_amplitude = 0.1;
   std::string forcing = "implicit";    // implicit (exact flux) | parity (meanUevol.c:201-221)
   bool health_check = true;
+  // Failure handling (the reference only exit(1)'d the failing rank, check.cu).
+  int health_every = 100;              // steps between global NaN/Inf checks
+  std::string on_nan = "abort";        // abort | rollback (restore the last in-memory snapshot)
+  int snapshot_every = 0;              // rollback snapshots (0 = health_every)
+  int max_rollbacks = 3;
+  double rollback_cfl_factor = 0.5;    // cfl *= factor after each rollback
+  // Observability.
+  int spectra_every = 0;               // 0 = off; 1-D kx/kz energy spectra + 2-D map (statistics.cu:245-326)
+  std::string spectra_planes = "";     // comma-separated y indices ("" = NY/2)
+  std::string log_json = "";           // JSON-lines run log path ("" = off)
 
   static Config from_tree(const ConfigTree& t);
   static Config from_file(const std::string& path, const std::vector<std::string>& overrides = {});
@@ -76,6 +86,7 @@ struct Config {
 
   int nzp() const { return 2 * NZ - 2; }
   bool fp64() const { return precision == "fp64"; }
+  std::vector<int> spectra_plane_list() const;   // parsed spectra_planes (default {NY/2})
 };
 
 }  // namespace channel

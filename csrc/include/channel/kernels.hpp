@@ -144,4 +144,20 @@ void dt_update(const DtArgs& a, hipStream_t s);
 // kz=0 plane Hermitian symmetrisation of a [y][nkx][nkz] field held entirely by one rank
 void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStream_t s);
 
+// ---- diagnostics ---------------------------------------------------------------------------
+struct SpectraArgs {
+  const void *u = nullptr, *v = nullptr, *w = nullptr;  // spectral [NY][lines], lines = nkx_loc*nkz_loc
+  int lines = 0, nkx_loc = 0, kx0 = 0, nkz_loc = 0, kz0 = 0;
+  int nkx = 0, Kx = 0, nkz = 0;       // global retained counts
+  const int* planes = nullptr;        // device [nplanes] y indices
+  int nplanes = 0;
+  double* ekx = nullptr;              // [3][nplanes][Kx+1]  (|kx| bins, summed over kz)
+  double* ekz = nullptr;              // [3][nplanes][nkz]   (summed over kx)
+  double* map = nullptr;              // [3][nkx][nkz] |q|^2 at planes[0] (may be null)
+};
+// accumulates (+=) into ekx/ekz; map is overwritten for the local block
+void spectra_accumulate(const SpectraArgs& a, bool fp64, hipStream_t s);
+// fault injection (tests): element `elem` of a complex field becomes NaN
+void inject_nan(void* field, size_t elem, bool fp64, hipStream_t s);
+
 }  // namespace channel

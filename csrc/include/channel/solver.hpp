@@ -82,6 +82,23 @@ class Solver {
   std::vector<double> kspec_profile();
   void symmetrize();                  // kz=0 Hermitian symmetry (P == 1 only)
 
+  // ---- failure handling -------------------------------------------------------
+  void take_snapshot();               // device copy of (phi, omega+U, dt, time, step)
+  void rollback();                    // restore it; cfl *= rollback_cfl_factor; re-capture graphs
+  long snapshot_step() const { return snap_step_; }
+  int rollbacks() const { return rollbacks_; }
+  double cfl() const { return cfg_.cfl; }
+  void inject_nan(int field = PHI);   // fault injection (tests)
+
+  // ---- diagnostics ---------------------------------------------------------------------------
+  // energy spectra of u,v,w of the current state at cfg.spectra_planes (global sums):
+  // ekx [3][np][Kx+1], ekz [3][np][nkz], map [3][nkx][nkz] at the first plane
+  struct Spectra {
+    std::vector<int> planes;
+    std::vector<double> ekx, ekz, map;
+  };
+  Spectra spectra();
+
   // ---- restart files (reference-compatible, Appendix B) --------------------------------
   void write_restart(const std::string& g, const std::string& ddv, const std::string& umean);
   void read_restart(const std::string& g, const std::string& ddv, const std::string& umean);
@@ -107,6 +124,10 @@ class Solver {
   void ev(int phase, bool end);
   void write_logs(const StepLog& L, bool verbose);
   void write_stats_files(const std::vector<double>& st);
+  void write_spectra_files(const Spectra& sp);
+  void write_json(const StepLog& L, double ms_per_step);
+  void wait(hipStream_t s);           // stream sync with the communicator watchdog (P > 1)
+  void invalidate_graphs();
 
   Config cfg_;
   Plan plan_;
@@ -144,6 +165,15 @@ class Solver {
   std::vector<hipEvent_t> ph_ev_;
   std::vector<double> ph_ms_;
   bool phase_timing_ = false;
+
+  // rollback snapshot
+  void* snap_ = nullptr;
+  long snap_step_ = -1;
+  int rollbacks_ = 0;
+  // spectra accumulators [ekx | ekz | map] and plane list (device)
+  void* d_spec_ = nullptr;
+  size_t spec_n_ = 0;
+  double comm_timeout_s_ = 900.0;     // CHANNEL_COMM_TIMEOUT_S (0 = wait forever)
 
   bool use_graph_ = true;
   bool graph_ok_[2] = {false, false};

@@ -76,4 +76,70 @@ void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStre
   HIP_LAUNCH_CHECK(s);
 }
 
+// Energy spectra of u, v, w at selected y planes (the reference's calcSpectra, statistics.cu:245-326,
+// is dead code that dumped |q|^2 of one plane; here it is a live, device-side diagnostic).
+// One block per (local kx, plane); fluctuations only (the (0,0) line carries U(y)).  The kz = 0
+// column counts once and kz > 0 twice (the -kz half), so E_kx sums to the plane energy.
+template <typename T2>
+__global__ void __launch_bounds__(256) spectra_kernel(SpectraArgs a) {
+  const int ikx = blockIdx.x, pl = blockIdx.y;
+  const int j = a.planes[pl];
+  const int ig = a.kx0 + ikx;
+  const int kx = ig <= a.Kx ? ig : ig - a.nkx;
+  const int akx = kx < 0 ? -kx : kx;
+  const T2* f[3] = {static_cast<const T2*>(a.u), static_cast<const T2*>(a.v), static_cast<const T2*>(a.w)};
+  double sx[3] = {0.0, 0.0, 0.0};
+  for (int kl = threadIdx.x; kl < a.nkz_loc; kl += blockDim.x) {
+    const int kz = a.kz0 + kl;
+    const size_t idx = static_cast<size_t>(j) * a.lines + static_cast<size_t>(ikx) * a.nkz_loc + kl;
+    const double wgt = (kx == 0 && kz == 0) ? 0.0 : (kz == 0 ? 1.0 : 2.0);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const T2 c = f[q][idx];
+      const double e = static_cast<double>(c.x) * c.x + static_cast<double>(c.y) * c.y;
+      sx[q] += wgt * e;
+      atomicAdd(&a.ekz[(static_cast<size_t>(q) * a.nplanes + pl) * a.nkz + kz], wgt * e);
+      if (pl == 0 && a.map) a.map[(static_cast<size_t>(q) * a.nkx + ig) * a.nkz + kz] = (kx == 0 && kz == 0) ? 0.0 : e;
+    }
+  }
+  __shared__ double red[3][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    double v = sx[q];
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[q][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int q = threadIdx.x;
+    double v = 0.0;
+    for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) v += red[q][i];
+    atomicAdd(&a.ekx[(static_cast<size_t>(q) * a.nplanes + pl) * (a.Kx + 1) + akx], v);
+  }
+}
+
+void spectra_accumulate(const SpectraArgs& a, bool fp64, hipStream_t s) {
+  CH_CHECK(a.nplanes > 0 && a.nkx_loc > 0 && a.nkz_loc > 0, "spectra: empty");
+  dim3 grid(a.nkx_loc, a.nplanes);
+  if (fp64) hipLaunchKernelGGL(spectra_kernel<double2>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(spectra_kernel<float2>, grid, dim3(256), 0, s, a);
+  HIP_LAUNCH_CHECK(s);
+}
+
+// fault injection (tests): overwrite one element of a field with NaN
+__global__ void poison_kernel(float* p) { p[0] = __int_as_float(0x7fc00000); }
+
+void inject_nan(void* field, size_t elem, bool fp64, hipStream_t s) {
+  char* b = static_cast<char*>(field) + elem * (fp64 ? 16 : 8);
+  if (fp64) {
+    const double nanv = std::nan("");
+    HIP_CHECK(hipMemcpyAsync(b, &nanv, sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  } else {
+    hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(1), 0, s, reinterpret_cast<float*>(b));
+    HIP_LAUNCH_CHECK(s);
+  }
+}
+
 }  // namespace channel

@@ -78,3 +78,17 @@ def test_invalid(native, bad):
 def test_input_files_imply_file_ic(native):
     c = native.Config.from_string('NX=32; NY=33; NZ=17; input: { G = "g.h5"; DDV = "d.h5"; };')
     assert c.ic == "file"
+
+
+def test_failure_and_observability_keys(native):
+    c = native.Config.from_string('NX=32; NY=33; NZ=17; on_nan = "rollback"; health_every = 5; snapshot_every = 20;'
+                                  ' max_rollbacks = 2; rollback_cfl_factor = 0.25; spectra_every = 50;'
+                                  ' spectra_planes = "16, 3"; log_json = "run.jsonl";')
+    assert (c.on_nan, c.health_every, c.snapshot_every, c.max_rollbacks) == ("rollback", 5, 20, 2)
+    assert c.rollback_cfl_factor == 0.25 and c.spectra_every == 50 and c.spectra_planes == "16, 3"
+    assert c.log_json == "run.jsonl"
+    again = native.Config.from_string(c.to_string())
+    assert again.on_nan == "rollback" and again.spectra_planes == "16, 3"
+    for bad in ['on_nan = "retry";', 'spectra_planes = "40";', 'spectra_planes = "a";', "health_every = 0;"]:
+        with pytest.raises(RuntimeError):
+            native.Config.from_string("NX=32; NY=33; NZ=17; " + bad)

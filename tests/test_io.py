@@ -52,3 +52,23 @@ def test_umean_format(native, tmp_path):
 def test_missing_file_raises(h5, tmp_path):
     with pytest.raises(RuntimeError):
         h5.h5_read_planes(str(tmp_path / "nope.h5"), [0])
+
+
+def test_truncated_checkpoint_raises(h5, tmp_path):
+    """Fault injection: a checkpoint cut short (e.g. the writer died) must fail loudly, not load garbage."""
+    NX, NY, NZ = 16, 9, 5
+    path = str(tmp_path / "G.h5")
+    h5.h5_create_field(path, NX, NY, NZ, False)
+    h5.h5_write_planes(path, list(range(NX)), list(np.ones(NX * NY * 2 * NZ)))
+    size = os.path.getsize(path)
+    with open(path, "r+b") as f:
+        f.truncate(size // 2)
+    with pytest.raises(RuntimeError):
+        h5.h5_read_planes(path, list(range(NX)))
+
+
+def test_garbage_checkpoint_raises(h5, tmp_path):
+    path = tmp_path / "DDV.h5"
+    path.write_bytes(b"not an hdf5 file" * 64)
+    with pytest.raises(RuntimeError):
+        h5.h5_read_planes(str(path), [0])
