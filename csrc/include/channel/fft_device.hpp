@@ -7,7 +7,7 @@
 // (34 dwords), which is conflict-free for ds_write_b64, and the strided reads stay contiguous.
 // Radix plans: 16, 16x2, 16x4, 16x8, 16x16, 16x16x2, 16x16x4, 16x16x8 (N = 16 ... 2048): at most
 // three LDS round trips per transform (the radix-4-only version needed log4 N + 1).
-// Twiddles W_N^m = exp(-2 pi i m / N) come from a global table (L1/L2 resident).
+// Twiddles come from per-pass tables (FftPlan::T1/T2, built by fft_twiddle_fill), staged in LDS.
 //
 // Replaces the reference's cuFFT 2-D plans (fft.c:17-23); length is a compile-time power of two.
 #pragma once
@@ -145,49 +145,6 @@ __device__ __forceinline__ void dftR(T2* v) {
   else dft16<INV>(v);
 }
 
-// ---- one Stockham pass --------------------------------------------------------------------
-template <int N, int R, int NS, int ROWS, int PITCH, int NT, bool INV, typename T2>
-__device__ __forceinline__ void stockham_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int tid) {
-  constexpr int Q = N / R;
-  constexpr int NB = ROWS * Q;
-  constexpr int B = (NB + NT - 1) / NT;
-  T2 v[B][R];
-#pragma unroll
-  for (int b = 0; b < B; ++b) {
-    const int idx = tid + b * NT;
-    if (NB % NT == 0 || idx < NB) {
-      const int row = idx / Q, j = idx - row * Q;
-      const T2* p = buf + row * PITCH;
-#pragma unroll
-      for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(j + r * Q)];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int b = 0; b < B; ++b) {
-    const int idx = tid + b * NT;
-    if (NB % NT == 0 || idx < NB) {
-      const int row = idx / Q, j = idx - row * Q;
-      const int k = j & (NS - 1);
-      if constexpr (NS > 1) {
-        constexpr int stride = N / (R * NS);
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-          T2 w = tw[k * r * stride];
-          if (INV) w.y = -w.y;
-          v[b][r] = cmul(v[b][r], w);
-        }
-      }
-      dftR<R, INV>(v[b]);
-      T2* p = buf + row * PITCH;
-      const int base = (j - k) * R + k;
-#pragma unroll
-      for (int r = 0; r < R; ++r) p[fft_pidx(base + r * NS)] = v[b][r];
-    }
-  }
-  __syncthreads();
-}
-
 // radix plan: 16 first, then 16, then the remainder
 template <int N>
 struct FftPlan {
@@ -197,15 +154,36 @@ struct FftPlan {
   static constexpr int R2 = N / (R0 * R1) > 1 ? N / (R0 * R1) : 1;
   static_assert(R0 * R1 * R2 == N, "unsupported FFT length");
   static_assert(R2 <= 16, "FFT length too large");
+  // per-pass twiddle tables, [r-1][k] (k = butterfly phase, fastest): for a fixed r the lanes of a
+  // wave read consecutive entries, which is bank-conflict free (the former single W_N^m table
+  // was read at k*r*stride, up to 16-way conflicts for even r)
+  static constexpr int T1 = R1 > 1 ? (R1 - 1) * R0 : 0;         // pass 2: NS = R0
+  static constexpr int T2 = R2 > 1 ? (R2 - 1) * R0 * R1 : 0;    // pass 3: NS = R0*R1
+  static constexpr int TSIZE = T1 + T2 > 0 ? T1 + T2 : 1;
 };
 
-// Rows are at buf + row*PITCH, element x of a row at fft_pidx(x).  Ends with a barrier.
-template <int N, int ROWS, int PITCH, int NT, bool INV, typename T2>
-__device__ void lds_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int tid) {
-  using Pl = FftPlan<N>;
-  stockham_pass<N, Pl::R0, 1, ROWS, PITCH, NT, INV>(buf, tw, tid);
-  if constexpr (Pl::R1 > 1) stockham_pass<N, Pl::R1, Pl::R0, ROWS, PITCH, NT, INV>(buf, tw, tid);
-  if constexpr (Pl::R2 > 1) stockham_pass<N, Pl::R2, Pl::R0 * Pl::R1, ROWS, PITCH, NT, INV>(buf, tw, tid);
+// host-side table builder: entry [(r-1)*NS + k] of a pass = W_N^(k*r*N/(R*NS)) = exp(-2 pi i ...)
+inline int fft_twiddle_size(int n) {
+  int r0 = n >= 16 ? 16 : n;
+  int r1 = n >= 256 ? 16 : (n / r0 > 1 ? n / r0 : 1);
+  int r2 = n / (r0 * r1) > 1 ? n / (r0 * r1) : 1;
+  int t = (r1 > 1 ? (r1 - 1) * r0 : 0) + (r2 > 1 ? (r2 - 1) * r0 * r1 : 0);
+  return t > 0 ? t : 1;
+}
+template <typename F>
+inline void fft_twiddle_fill(int n, F&& put) {  // put(index, m): entry index holds W_n^m
+  int r0 = n >= 16 ? 16 : n;
+  int r1 = n >= 256 ? 16 : (n / r0 > 1 ? n / r0 : 1);
+  int r2 = n / (r0 * r1) > 1 ? n / (r0 * r1) : 1;
+  int off = 0;
+  auto pass = [&](int R, int NS) {
+    const int stride = n / (R * NS);
+    for (int r = 1; r < R; ++r)
+      for (int k = 0; k < NS; ++k) put(off + (r - 1) * NS + k, k * r * stride);
+    off += (R - 1) * NS;
+  };
+  if (r1 > 1) pass(r1, r0);
+  if (r2 > 1) pass(r2, r0 * r1);
 }
 
 // ---- wave-owned variant -------------------------------------------------------------------
@@ -216,6 +194,7 @@ __device__ void lds_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int tid
 // global<->LDS staging, not per pass.
 template <int N, int R, int NS, int RW, int PITCH, bool INV, typename T2>
 __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
+  // tw: this pass's [R-1][NS] twiddle table
   constexpr int Q = N / R;
   constexpr int NB = RW * Q;
   constexpr int B = (NB + 63) / 64;
@@ -238,10 +217,9 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       const int row = idx / Q, j = idx - row * Q;
       const int k = j & (NS - 1);
       if constexpr (NS > 1) {
-        constexpr int stride = N / (R * NS);
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          T2 w = tw[k * r * stride];
+          T2 w = tw[(r - 1) * NS + k];
           if (INV) w.y = -w.y;
           v[b][r] = cmul(v[b][r], w);
         }
@@ -261,7 +239,7 @@ __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restr
   using Pl = FftPlan<N>;
   wave_pass<N, Pl::R0, 1, RW, PITCH, INV>(buf, tw, lane);
   if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV>(buf, tw, lane);
-  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw, lane);
+  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw + Pl::T1, lane);
 }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for vmcnt(0), i.e. for

@@ -68,7 +68,7 @@ constexpr int kKspecPhases = 10;
 void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream);
 
 // ---- FFT stages ---------------------------------------------------------------------------
-// Twiddle table for length n (double and float copies): W_n^m = exp(-2 pi i m / n), m < n.
+// Per-pass FFT twiddle tables for length n (FftPlan T1/T2 layout, fft_device.hpp), fp32 or fp64.
 struct Twiddles {
   void* buf = nullptr;
   int n = 0;
@@ -103,6 +103,7 @@ struct XArgs {
   int npseg = 1;
   int x_start[9] = {0};
   long long poff[8] = {0};
+  int diag = 0;                      // bit 0: skip the transforms (timing diagnosis, CHANNEL_FFT_DIAG)
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
@@ -116,6 +117,7 @@ struct ZArgs {
   int nseg = 1;
   int kz_start[9] = {0};
   long long off[8] = {0};
+  int diag = 0;                      // bit 0: skip the transforms (timing diagnosis)
   long long field_stride = 0;        // element stride between the 6 input fields
   double scale = 1.0;                // forward normalisation 1/(NX*Nzp)
   const double* inv_dy = nullptr;    // [NY] 1/local spacing for the CFL estimate

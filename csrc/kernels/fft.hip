@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "channel/common.hpp"
@@ -31,17 +32,17 @@ void Twiddles::build(int n_, bool fp64_) {
   n = n_;
   fp64 = fp64_;
   const double two_pi = 2.0 * std::acos(-1.0);
+  const int sz = fft_twiddle_size(n);
+  std::vector<double2> h(sz, double2{1.0, 0.0});
+  fft_twiddle_fill(n, [&](int i, int m) { h[i] = double2{std::cos(two_pi * m / n), -std::sin(two_pi * m / n)}; });
   if (fp64) {
-    std::vector<double2> h(n);
-    for (int m = 0; m < n; ++m) h[m] = double2{std::cos(two_pi * m / n), -std::sin(two_pi * m / n)};
-    HIP_CHECK(hipMalloc(&buf, n * sizeof(double2)));
-    HIP_CHECK(hipMemcpy(buf, h.data(), n * sizeof(double2), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMalloc(&buf, sz * sizeof(double2)));
+    HIP_CHECK(hipMemcpy(buf, h.data(), sz * sizeof(double2), hipMemcpyHostToDevice));
   } else {
-    std::vector<float2> h(n);
-    for (int m = 0; m < n; ++m)
-      h[m] = float2{static_cast<float>(std::cos(two_pi * m / n)), static_cast<float>(-std::sin(two_pi * m / n))};
-    HIP_CHECK(hipMalloc(&buf, n * sizeof(float2)));
-    HIP_CHECK(hipMemcpy(buf, h.data(), n * sizeof(float2), hipMemcpyHostToDevice));
+    std::vector<float2> hf(sz);
+    for (int i = 0; i < sz; ++i) hf[i] = float2{static_cast<float>(h[i].x), static_cast<float>(h[i].y)};
+    HIP_CHECK(hipMalloc(&buf, sz * sizeof(float2)));
+    HIP_CHECK(hipMemcpy(buf, hf.data(), sz * sizeof(float2), hipMemcpyHostToDevice));
   }
 }
 
@@ -52,23 +53,55 @@ void Twiddles::release() {
 
 // ---- x-direction -------------------------------------------------------------------------
 constexpr int xcfg_c(int nx, int tsz) { return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 1024 ? 4 : 8); }
-constexpr int xcfg_nt(int nx, int tsz) { return 256 + 0 * nx * tsz; }
-
-template <int NX, typename T>
+// WIDE = 1: twice the kz columns per tile (128-B row segments) with 512 threads and one block per
+// CU (the same 8 waves per CU); WIDE = 0: 64-B segments, 256 threads, two blocks per CU.
+constexpr int xcfg_nt(int wide) { return wide ? 512 : 256; }
+constexpr int xcfg_minb(int wide) { return wide ? 1 : 2; }
+template <int NX, typename T, int WIDE = 0>
 struct XCfg {
-  // kz columns per tile (64-B segments; 128-B tiles measured slower: 1 block/CU)
-  static constexpr int C = xcfg_c(NX, sizeof(T));
-  static constexpr int NT = xcfg_nt(NX, sizeof(T));
+  // kz columns per tile
+  static constexpr int C = xcfg_c(NX, sizeof(T)) * (WIDE ? 2 : 1);
+  static constexpr int NT = xcfg_nt(WIDE);
   // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
   // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
   static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
 };
 
-__device__ __forceinline__ int find_block(const int* start, int n, int i) {
-  int s = 0;
-  for (int q = 1; q < n; ++q)
-    if (i >= start[q]) s = q;
-  return s;
+// CHANNEL_FFT_DIAG=1 skips the in-LDS transforms (timing diagnosis only: results are wrong)
+static int fft_diag() {
+  static const int d = [] {
+    const char* e = std::getenv("CHANNEL_FFT_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return d;
+}
+
+static bool xwide_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_XWIDE");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
+// Segment lookup in a small split table (at most MAXS segments) without dynamic indexing.
+// Indexing a by-value kernel-argument array with a per-lane index makes hipcc gather the entries
+// from the kernarg segment with per-lane global loads, each followed by s_waitcnt vmcnt(0): that
+// drained every in-flight prefetch load and store of the wave at every element and serialised
+// the x transforms.  Unrolled over the compile-time capacity the entries are wave-uniform
+// (SGPR) values and the lookup is a chain of compares and selects.
+struct SegPos {
+  int start;      // first index of the segment
+  int count;      // its length
+  long long off;  // element offset of its block
+};
+template <int MAXS = 8>
+__device__ __forceinline__ SegPos seg_find(const int* start, const long long* off, int n, int i) {
+  SegPos p{start[0], start[1] - start[0], off[0]};
+#pragma unroll
+  for (int q = 1; q < MAXS; ++q)
+    if (q < n && i >= start[q]) p = SegPos{start[q], start[q + 1] - start[q], off[q]};
+  return p;
 }
 
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
@@ -76,18 +109,19 @@ __device__ __forceinline__ int find_block(const int* start, int n, int i) {
 // into registers right after the current tile is staged into LDS, so they are in flight during
 // the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
-template <int NX, typename T, bool SEG>
-__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys,
-                                                            const typename C2<T>::type* tw) {
+template <int NX, typename T, bool SEG, int WIDE>
+__global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
+    xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
-  using Cfg = XCfg<NX, T>;
+  using Cfg = XCfg<NX, T, WIDE>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
   constexpr int NKMAX = 2 * (NX / 3) + 1;
   constexpr int EPT = (NKMAX * C + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
-  __shared__ T2 tws[NX];
-  for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
+  constexpr int TS = FftPlan<NX>::TSIZE;
+  __shared__ T2 tws[TS];
+  for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const int ntiles = a.ny * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
@@ -102,15 +136,13 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int i = e / C, c = e - i * C;
-      const int kz = kz0 + c;
-      v[q] = T2{0, 0};
-      if (e < nload && kz < a.nkz) {
-        const int sb = find_block(src.kx_start, src.nsrc, i);
-        const int nk = src.kx_start[sb + 1] - src.kx_start[sb];
-        // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
-        v[q] = base[static_cast<unsigned>(src.off[sb] + (static_cast<long long>(y) * nk + (i - src.kx_start[sb])) * a.nkz + kz)];
-      }
+      // unconditional load from a clamped valid address: rows i >= nkx are never staged,
+      // columns kz >= nkz are transformed (independently) but never stored
+      const int i = min(e / C, a.nkx - 1);
+      const int kz = min(kz0 + e % C, a.nkz - 1);
+      const SegPos sp = seg_find(src.kx_start, src.off, src.nsrc, i);
+      // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
+      v[q] = base[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
     }
   };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
@@ -135,8 +167,9 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
     {
       constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
       // one row at a time: the prefetched next tile already holds EPT registers
+      if (!(a.diag & 1))
 #pragma unroll 1
-      for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, true>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+        for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, true>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
@@ -145,27 +178,28 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_backward_kerne
       const int kz = kz0 + c;
       if (kz < a.nkz) {
         if constexpr (SEG) {
-          const int d = find_block(a.x_start, a.npseg, x);
-          const int nxd = a.x_start[d + 1] - a.x_start[d];
-          out[a.poff[d] + (static_cast<long long>(y) * nxd + (x - a.x_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+          out[sp.off + (static_cast<long long>(y) * sp.count + (x - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
         } else {
-          out[(static_cast<long long>(y) * NX + x) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+          out[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
+              s[c * PITCH + fft_pidx(x)];
         }
       }
     }
   }
 }
 
-template <int NX, typename T, bool SEG>
-__global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst,
-                                                           const typename C2<T>::type* tw) {
+template <int NX, typename T, bool SEG, int WIDE>
+__global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
+    xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
-  using Cfg = XCfg<NX, T>;
+  using Cfg = XCfg<NX, T, WIDE>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   constexpr int EPT = (NX * C + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
-  __shared__ T2 tws[NX];
-  for (int i = threadIdx.x; i < NX; i += NT) tws[i] = tw[i];
+  constexpr int TS = FftPlan<NX>::TSIZE;
+  __shared__ T2 tws[TS];
+  for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const int ntiles = a.ny * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
@@ -178,18 +212,14 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int x = e / C, c = e - x * C;
-      const int kz = kz0 + c;
-      v[q] = T2{0, 0};
-      if (e < NX * C && kz < a.nkz) {
-        if constexpr (SEG) {
-          const int d = find_block(a.x_start, a.npseg, x);
-          const int nxd = a.x_start[d + 1] - a.x_start[d];
-          v[q] = in[static_cast<unsigned>(a.poff[d]) +
-                    static_cast<unsigned>(y * nxd + x - a.x_start[d]) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
-        } else {
-          v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
-        }
+      const int x = min(e / C, NX - 1);
+      const int kz = min(kz0 + e % C, a.nkz - 1);
+      if constexpr (SEG) {
+        const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+        v[q] = in[static_cast<unsigned>(sp.off) +
+                  static_cast<unsigned>(y * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      } else {
+        v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
       }
     }
   };
@@ -210,8 +240,9 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
     {
       constexpr int RW = C / (NT / 64);
       // one row at a time: the prefetched next tile already holds EPT registers
+      if (!(a.diag & 1))
 #pragma unroll 1
-      for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, false>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+        for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, false>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
@@ -220,9 +251,8 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
       const int kz = kz0 + c;
       if (kz < a.nkz) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
-        const int d = find_block(dst.kx_start, dst.ndst, i);
-        const int nk = dst.kx_start[d + 1] - dst.kx_start[d];
-        outb[dst.off[d] + (static_cast<long long>(y) * nk + (i - dst.kx_start[d])) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        const SegPos sp = seg_find(dst.kx_start, dst.off, dst.ndst, i);
+        outb[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
       }
     }
   }
@@ -241,19 +271,37 @@ __global__ void __launch_bounds__(xcfg_nt(NX, sizeof(T)), 2) xfft_forward_kernel
     default: CH_CHECK(false, "unsupported FFT length " << N_); \
   }
 
+template <int NN, typename T, int WIDE>
+static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NN, T, WIDE>;
+  auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true, WIDE> : xfft_backward_kernel<NN, T, false, WIDE>;
+  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
+}
+
+template <int NN, typename T, int WIDE>
+static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NN, T, WIDE>;
+  auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true, WIDE> : xfft_forward_kernel<NN, T, false, WIDE>;
+  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
+                     static_cast<const T2*>(tw.buf));
+}
+
 template <typename T>
 static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
-  using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
     if constexpr (sizeof(T) == 8 && NN > 1024) {
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
+    } else if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
+      if (xwide_enabled()) xb_launch_cfg<NN, T, 1>(a, src, phys, tw, s);
+      else xb_launch_cfg<NN, T, 0>(a, src, phys, tw, s);
     } else {
-      constexpr int C = XCfg<NN, T>::C;
-      auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true> : xfft_backward_kernel<NN, T, false>;
-      const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
-      dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
-      hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, src, static_cast<T2*>(phys),
-                         static_cast<const T2*>(tw.buf));
+      xb_launch_cfg<NN, T, 0>(a, src, phys, tw, s);
     }
   });
   HIP_LAUNCH_CHECK(s);
@@ -261,17 +309,14 @@ static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddle
 
 template <typename T>
 static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
-  using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.NX, {
     if constexpr (sizeof(T) == 8 && NN > 1024) {
       CH_CHECK(false, "fp64 storage supports NX <= 1024");
+    } else if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
+      if (xwide_enabled()) xf_launch_cfg<NN, T, 1>(a, phys, dst, tw, s);
+      else xf_launch_cfg<NN, T, 0>(a, phys, dst, tw, s);
     } else {
-      constexpr int C = XCfg<NN, T>::C;
-      auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true> : xfft_forward_kernel<NN, T, false>;
-      const int ntiles = a.ny * ((a.nkz + C - 1) / C) * a.nfields;
-      dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), XCfg<NN, T>::NT)));
-      hipLaunchKernelGGL(kern, grid, dim3(XCfg<NN, T>::NT), 0, s, a, static_cast<const T2*>(phys), dst,
-                         static_cast<const T2*>(tw.buf));
+      xf_launch_cfg<NN, T, 0>(a, phys, dst, tw, s);
     }
   });
   HIP_LAUNCH_CHECK(s);
@@ -280,6 +325,7 @@ static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const T
 // one segment: plain [y][x][kz]; otherwise the table must tile [0, NX)
 static XArgs norm_pseg(const XArgs& in) {
   XArgs a = in;
+  a.diag = fft_diag();
   if (a.npseg <= 1) {
     a.npseg = 1;
     a.x_start[0] = 0;
@@ -296,6 +342,7 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
   CH_CHECK(a.nkx <= 2 * (a.NX / 3) + 1, "xfft_backward: more retained kx than the 2/3 rule allows");
   CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
+  CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_backward: per-field plane block exceeds 32-bit offsets");
   if (fp64) xb_launch<double>(a, src, phys, tw, s);
   else xb_launch<float>(a, src, phys, tw, s);
 }
@@ -325,10 +372,11 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   constexpr int PITCH = FftPitch<NZP>::value;
   constexpr int EP = (NZP + 63) / 64;  // points per lane
   __shared__ T2 s[ZW * PITCH];
-  __shared__ T2 tws[NZP];  // twiddles staged once per block: LDS latency instead of L2 in the passes
+  constexpr int TS = FftPlan<NZP>::TSIZE;
+  __shared__ T2 tws[TS];  // twiddles staged once per block: LDS latency instead of L2 in the passes
   __shared__ float red[4][ZW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < NZP; i += ZW * 64) tws[i] = tw[i];
+  for (int i = tid; i < TS; i += ZW * 64) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
@@ -339,8 +387,8 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz)
   auto zaddr = [&](int k) -> long long {
     if constexpr (SEG) {
-      const int sb = find_block(a.kz_start, a.nseg, k);
-      return a.off[sb] + r * (a.kz_start[sb + 1] - a.kz_start[sb]) + (k - a.kz_start[sb]);
+      const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
+      return sp.off + r * sp.count + (k - sp.start);
     } else {
       return r * nkz + k;
     }
@@ -377,7 +425,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
       }
       for (int k = Kz + 1 + lane; k < NZP - Kz; k += 64) row[fft_pidx(k)] = T2{0, 0};
       __builtin_amdgcn_wave_barrier();
-      wave_fft<NZP, 1, PITCH, true>(row, tws, lane);
+      if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, true>(row, tws, lane);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
         const int n = lane + 64 * i;
@@ -404,13 +452,30 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
     }
     __builtin_amdgcn_wave_barrier();
     const T sc = static_cast<T>(0.5 * a.scale);
-    wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
+    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
-    for (int k = lane; k < nkz; k += 64) {
-      const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
-      const long long o = zaddr(k);
-      fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
-      fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+    // (unrolled: all LDS reads are issued before the global stores)
+    constexpr int MKO = (NZP / 2 + 63) / 64;
+    {
+      T2 z0[MKO], z1[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx((NZP - k) & (NZP - 1))];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          const T2 Z = z0[i], Zm = z1[i];
+          const long long o = zaddr(k);
+          fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+          fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+        }
+      }
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -419,10 +484,22 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
       if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
     }
     __builtin_amdgcn_wave_barrier();
-    wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
-    for (int k = lane; k < nkz; k += 64) {
-      const T2 Z = row[fft_pidx(k)], Zm = row[fft_pidx((NZP - k) & (NZP - 1))];
-      fields[2 * fs + zaddr(k)] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
+    {
+      T2 z0[MKO], z1[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx((NZP - k) & (NZP - 1))];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
+      }
     }
   }
   // block maxima -> one atomicMax per block and quantity
@@ -468,6 +545,7 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
 
 void zphys(const ZArgs& a_in, void* fields, const Twiddles& tw, bool fp64, hipStream_t s) {
   ZArgs a = a_in;
+  a.diag = fft_diag();
   if (a.nseg <= 1) {
     a.nseg = 1;
     a.kz_start[0] = 0;
