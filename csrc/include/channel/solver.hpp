@@ -158,6 +158,7 @@ class Solver {
   unsigned* d_health_ = nullptr;
   unsigned long long* d_kprof_ = nullptr;
   bool kprof_on_ = false;
+  int ystreams_ = 1;               // streams the y chunks alternate over
   int ychunk_ = 0;                 // y planes per x->z->x pipeline chunk (P = 1), 0 = whole slab
   double* d_invdy_ = nullptr;
 

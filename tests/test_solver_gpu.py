@@ -91,14 +91,15 @@ def test_graph_equals_eager_fp32(native):
     assert np.isfinite(pa).all() and a.health() == 0
 
 
-@pytest.mark.parametrize("chunk", [1, 7, 16])
-def test_ychunk_pipeline_equals_whole_slab(native, monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,streams", [(1, 1), (7, 1), (16, 1), (7, 2), (8, 2)])
+def test_ychunk_pipeline_equals_whole_slab(native, monkeypatch, chunk, streams):
     """The y-chunked x->z->x pipeline (P = 1) is bitwise the whole-slab one, ragged last chunk included."""
     kw = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp32", ic="random", ic_amplitude=0.2, stats_every=0,
               log_every=0, symmetry_every=0)
     monkeypatch.setenv("CHANNEL_YCHUNK", "0")
     a = make_solver(native, **kw)
     monkeypatch.setenv("CHANNEL_YCHUNK", str(chunk))
+    monkeypatch.setenv("CHANNEL_YSTREAMS", str(streams))
     b = make_solver(native, **kw)
     for s in (a, b):
         s.init_ic()

@@ -95,7 +95,7 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
             f.result()
     if _stale(CORE_SO, objs, 0.0):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", CORE_SO, "-L/opt/rocm/lib", "-lrccl",
-              "-ldl", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-soname,libchannel_core.so"], verbose)
+              "-lrocprofiler-sdk-roctx", "-ldl", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-soname,libchannel_core.so"], verbose)
     # bindings
     bsrc = os.path.join(ROOT, "csrc", "bindings", "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
