@@ -80,7 +80,8 @@ def main() -> None:
     barrier()
     dt_wall = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt_wall], dtype=torch.float64, device="cuda")
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([dt_wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt_wall = float(t.item())
     L = solver.log()

@@ -4,12 +4,19 @@ One process per GPU (torchrun / torch.distributed.run).  The solver owns its own
 communicator (created in C++ with ncclCommInitRank) so its all-to-alls can be enqueued on its own
 streams and captured in its hipGraph; torch.distributed is only used to agree on the 128-byte
 ncclUniqueId (rank 0 creates it, broadcast_object_list distributes it) and for host-side barriers
-and timing reductions.  The reference bootstrapped nothing: it used host MPI for all data
+and timing reductions.  That control plane is gloo (CPU) by default: it moves a few bytes, and a
+second, torch-owned RCCL communicator per GPU would only cost HBM and init time.
+
+``CHANNEL_COMM=shm`` swaps the RCCL data plane for the shared-memory loopback communicator
+(ShmComm): same block addressing, host-staged copies.  It lets several ranks share one GPU (RCCL
+refuses that: "Duplicate GPU detected"), so the whole torchrun bench/driver path can be rehearsed
+on a one-GPU box.  The reference bootstrapped nothing: it used host MPI for all data
 movement (channel_cuda_mpi.c:64-128) and bound rank%2 to a device (main.c:87).
 """
 from __future__ import annotations
 
 import os
+import uuid
 
 import torch
 import torch.distributed as dist
@@ -28,13 +35,19 @@ def dist_info() -> tuple[int, int, int]:
 
 
 def nccl_unique_id() -> bytes:
-    """Create the RCCL unique id on rank 0 and share it with every rank (empty for 1 rank)."""
+    """Create the communicator id on rank 0 and share it with every rank (empty for 1 rank).
+
+    RCCL ncclUniqueId by default; a "shm:<name>" id when CHANNEL_COMM=shm."""
     rank, world, _ = dist_info()
     if world == 1:
         return b""
     if not dist.is_initialized():
         raise RuntimeError("world_size > 1 requires torch.distributed to be initialised")
-    obj = [require_native().new_unique_id() if rank == 0 else None]
+    if os.environ.get("CHANNEL_COMM", "rccl").lower() == "shm":
+        uid = f"shm:channel_{os.getpid()}_{uuid.uuid4().hex[:10]}".encode() if rank == 0 else None
+    else:
+        uid = require_native().new_unique_id() if rank == 0 else None
+    obj = [uid]
     dist.broadcast_object_list(obj, src=0)
     return obj[0]
 
@@ -44,7 +57,7 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
     world = int(os.environ.get("WORLD_SIZE", 1))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("CHANNEL_DIST_BACKEND", "gloo")
         dist.init_process_group(backend=backend)
     rank, world, local = dist_info()
     if torch.cuda.is_available():
