@@ -25,6 +25,9 @@ sys.path.insert(0, ROOT)
 
 # analytic K20X-class model floor of the reference at this grid, s per RK3 step
 REF_MODEL_FLOOR_S = {1: 23.5, 2: 11.8, 4: 6.0, 8: 3.0}
+# BASELINE.json configs by grid (NX, NY, Nz_physical)
+RE_TAU_LABEL = {(32, 33, 32): "laminar Poiseuille", (128, 129, 128): "Re_tau~180", (512, 257, 512): "Re_tau~550",
+                (1024, 385, 1024): "Re_tau~950", (2048, 633, 2048): "Re_tau~2000"}
 
 
 def main() -> None:
@@ -106,7 +109,7 @@ def main() -> None:
         "dtype": "fp32 storage, fp64 y-solves" if args.precision == "fp32" else args.precision,
         "data": "synthetic (seeded random divergence-free IC on the laminar profile)",
         "config": {
-            "model": f"channel DNS Re_tau~950 (Re={args.re:g}, Q=1.8, LX=2pi, LZ=pi)",
+            "model": f"channel DNS {RE_TAU_LABEL.get((NX, NY, NZP), 'custom grid')} (Re={args.re:g}, Q=1.8, LX=2pi, LZ=pi)",
             "grid": f"{NX}x{NY}x{NZP}",
             "global_batch": 1,
             "seq_len": pts,
