@@ -150,8 +150,14 @@ void Solver::alloc() {
   kprof_on_ = std::getenv("CHANNEL_KSPEC_PROF") != nullptr;
   // y planes per x->z->x chunk (P = 1): 16 planes of 6 fp32 fields at NX = Nzp = 1024 are ~270 MB,
   // about the Infinity Cache; measured 57.9 -> 52.3 ms/step at 1024x385x1024 (4..64 swept, 16 best
-  // on one stream); alternating two streams with 8-plane chunks: 50.6 ms/step
-  ychunk_ = 8;
+  // on one stream); alternating two streams with 8-plane chunks: 50.6 ms/step.  The chunk is sized
+  // in bytes (~144 MiB of x-expanded intermediates per stream), which the sweeps confirm across
+  // grids: 512x257x512 best at 32 planes (11.2 -> 10.1 ms), 1024^2 fp64 at 4, 2048x633x2048 at 2
+  // (gpurun_out/yc_*, profiles/r01_v18_ychunk_sweep.log)
+  {
+    const size_t plane = 6ull * static_cast<size_t>(plan_.NX) * plan_.nkz * (fp64_ ? 16 : 8);
+    ychunk_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, (144ull << 20) / plane)));
+  }
   ystreams_ = 2;
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = std::atoi(yc);
   if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::atoi(ys);

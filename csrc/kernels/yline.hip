@@ -286,9 +286,16 @@ struct SpecTile {
   static constexpr int PITCH = W + 1;
   // r-planes padded by one slot so consecutive y rows (consecutive r) of a staging store differ in bank
   static constexpr int PLANE = 64 * PITCH + 1;
+  // Register slots hold R values per field per thread: at R <= 8 seven slots fit next to the
+  // solver state, at R = 10 they pushed the kernel to 970 spilled VGPRs (130 ms/substep at
+  // 2048x633x2048).  Above R = 8 a slot only records the field's address and commit() issues the
+  // loads (all R per thread back to back, then the LDS stores).
+  static constexpr bool kRegSlots = R <= 8;
   T2* tile;
   int N, lines, line0, w, lane;
-  T2 pend[NS][R];  // prefetch slots: this thread's share of fields whose loads are in flight
+  T2 pend[kRegSlots ? NS : 1][R];  // prefetch slots: this thread's share of fields whose loads are in flight
+  const T2* dsrc[kRegSlots ? 1 : NS];
+  int dl0[kRegSlots ? 1 : NS];
 
   // Issue the global loads of a field (N*W <= 64*R*W => at most R per thread) without waiting:
   // the kernel prefetches field k+1 before computing on field k, so at one wave per SIMD the HBM
@@ -297,6 +304,11 @@ struct SpecTile {
   __device__ void prefetch(const T2* __restrict__ src) { prefetch_at<S>(src, line0); }
   template <int S = 0>
   __device__ void prefetch_at(const T2* __restrict__ src, int l0) {
+    if constexpr (!kRegSlots) {
+      dsrc[S] = src;
+      dl0[S] = l0;
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int e = threadIdx.x + q * W * 64;
@@ -315,7 +327,13 @@ struct SpecTile {
       if (e < N * W) {
         const int y = e / W, l = e - y * W;
         const int ly = y / R, r = y - ly * R;
-        tile[r * PLANE + ly * PITCH + l] = pend[S][q];
+        if constexpr (kRegSlots) {
+          tile[r * PLANE + ly * PITCH + l] = pend[S][q];
+        } else {
+          const int l0 = dl0[S];
+          tile[r * PLANE + ly * PITCH + l] =
+              l0 + l < lines ? dsrc[S][static_cast<size_t>(y) * lines + l0 + l] : T2{0, 0};
+        }
       }
     }
     lds_barrier();
@@ -368,7 +386,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // ~500-cycle load at one wave per SIMD.  Offsets are compile-time so the reads stay ds_read.
   constexpr int ROWS = 64 * R;
   constexpr int NTAB = 14 * ROWS + PFac<R>::kNumFields * 64;
-  constexpr bool TLDS = NTAB * 8 <= 72 * 1024;
+  // stage when tables + the staging tile fit the 160 KB LDS with headroom (one block per CU at
+  // this register budget, so LDS does not limit occupancy): R <= 12 in fp32
+  constexpr bool TLDS = NTAB * 8 + R * (64 * (W + 1) + 1) * static_cast<int>(sizeof(T2)) <= 144 * 1024;
   __shared__ double tab_lds[TLDS ? NTAB : 1];
   YTab t = tg;
   if constexpr (TLDS) {

@@ -41,6 +41,32 @@ def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
         assert rel(gU, o.U) < 1e-11, f"U step {it}"
 
 
+@pytest.mark.parametrize("precision,NY", [("fp32", 385), ("fp32", 633), ("fp64", 633)])
+def test_gpu_matches_oracle_large_ny(native, precision, NY):
+    """Tall lines: R = 7 (register prefetch slots) and R = 10 (deferred slots, LDS-staged tables)."""
+    NX, NZ, dt = 16, 9, 1e-4
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision=precision, dt_fixed=dt, stats_every=0, log_every=0,
+              symmetry_every=0, ic="zero")
+    s = make_solver(native, **kw)
+    o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=dt)
+    phi, om = ora.random_state(o.plan, o.ops, seed=5, amp=0.05)
+    if precision == "fp32":
+        phi = phi.astype(np.complex64).astype(np.complex128)
+        om = om.astype(np.complex64).astype(np.complex128)
+    tol, tolU = (1e-9, 1e-11) if precision == "fp64" else (1e-4, 1e-5)  # fp32 storage round-off grows with NY
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    o.set_state(phi, om, U)
+    s.set_state(phi, om, U)
+    s.prepare()
+    for it in range(2):
+        o.step()
+        s.step(False)
+        gphi, gom, gU = s.get_state()
+        assert rel(gphi, o.phi) < tol, f"phi step {it}: {rel(gphi, o.phi):.3e}"
+        assert rel(gom, o.om) < tol, f"omega step {it}: {rel(gom, o.om):.3e}"
+        assert rel(gU, o.U) < tolU, f"U step {it}: {rel(gU, o.U):.3e}"
+
+
 def test_poiseuille_steady(native):
     """BASELINE config 1 on the GPU path: the laminar profile 1.35(1-y^2) is a steady state."""
     s = make_solver(native, NX=32, NY=33, NZ=17, Re=100.0, precision="fp64", ic="laminar", stats_every=0,
