@@ -290,9 +290,10 @@ struct SpecTile {
   // solver state, at R = 10 they pushed the kernel to 970 spilled VGPRs (130 ms/substep at
   // 2048x633x2048).  Above R = 8 a slot only records the field's address and commit() issues the
   // loads (all R per thread back to back, then the LDS stores).
-  // fp64: address-only at R = 3, 4 (W = 8; 128x129x128 fp64 1.18 -> 0.83 ms/step), register slots
-  // at R = 5..8 despite spills (1024x385x1024 fp64: 99.6 ms vs 105.7 ms address-only)
-  static constexpr bool kRegSlots = sizeof(T) == 4 ? R <= 8 : (R <= 2 || (R >= 5 && R <= 8));
+  // R = 3, 4 (W = 8 lines per block) spill with register slots too: address-only there
+  // (128x129x128 fp64 1.18 -> 0.84 ms/step); register slots at R = 5..8 despite some spills
+  // (1024x385x1024 fp64: 99.4 ms vs 105.7 ms address-only)
+  static constexpr bool kRegSlots = R <= 2 || (R >= 5 && R <= 8);
   T2* tile;
   int N, lines, line0, w, lane;
   T2 pend[kRegSlots ? NS : 1][R];  // prefetch slots: this thread's share of fields whose loads are in flight
