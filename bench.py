@@ -7,27 +7,61 @@ GPUs of one node with the slab decomposition (one rank per GPU, RCCL all-to-all 
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
 
+``--gpus N > 1`` without a torchrun environment launches itself under torch.distributed.run as a
+child process (before anything touches the GPU) and exits with its return code.
+
 Synthetic data: a seeded random divergence-free velocity field on a laminar mean profile
-(no checkpoint is available offline).  W untimed warm-up steps (graph capture happens there), then
-exactly K RK3 steps timed between barrier + device synchronisation on every rank; the MAX over
-ranks is reported.  Total work is fixed as N grows ("strong" scaling).
+(no checkpoint is available offline).  W untimed warm-up steps (the first one eager, then graph
+capture), then exactly K RK3 steps timed between barrier + device synchronisation on every rank;
+the MAX over ranks is reported.  Total work is fixed as N grows ("strong" scaling).  Per-step
+device times (hipEvents between graph launches) give the median and p90.  For P > 1 a few extra,
+untimed, eagerly-run steps with per-phase events give the exchange time and per-peer bandwidth.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# analytic K20X-class model floor of the reference at this grid (BASELINE.md §2), s per RK3 step
+# analytic K20X-class model floor of the reference at this grid (SURVEY §6.2; a model, not a
+# measurement: the reference publishes no numbers and cannot run this grid), s per RK3 step
 REF_MODEL_FLOOR_S = {1: 23.5, 2: 11.8, 4: 6.0, 8: 3.0}
 # BASELINE.json configs by grid (NX, NY, Nz_physical)
 RE_TAU_LABEL = {(32, 33, 32): "laminar Poiseuille", (128, 129, 128): "Re_tau~180", (512, 257, 512): "Re_tau~550",
                 (1024, 385, 1024): "Re_tau~950", (2048, 633, 2048): "Re_tau~2000"}
+# environment switches that skip work inside the timed region (diagnosis only)
+WORK_SKIPPING_ENV = ("CHANNEL_FFT_DIAG",)
+PHASES = ["kspec", "x_backward", "z_physical", "x_forward", "a2a", "reduce", "io", "other"]
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """Run this script under torch.distributed.run with n ranks (child process, no exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _pct(v: list[float], q: float) -> float:
+    s = sorted(v)
+    if not s:
+        return float("nan")
+    i = min(len(s) - 1, max(0, int(round(q * (len(s) - 1)))))
+    return s[i]
 
 
 def main() -> None:
@@ -41,13 +75,22 @@ def main() -> None:
     ap.add_argument("--decomposition", default="slab", choices=["slab", "pencil"])
     ap.add_argument("--pr", type=int, default=0, help="pencil rows (0 = automatic, most square)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--phases", action="store_true", help="per-phase timing (eager, synchronising)")
+    ap.add_argument("--phases", action="store_true",
+                    help="after the timed steps, time a few more eagerly with per-phase hipEvents")
+    ap.add_argument("--phase-steps", type=int, default=3)
     args = ap.parse_args()
+
+    bad = [e for e in WORK_SKIPPING_ENV if os.environ.get(e, "0") not in ("", "0")]
+    if bad:
+        raise SystemExit(f"refusing to benchmark with work-skipping diagnostics enabled: {bad}")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(_self_launch(args.gpus))
 
     import torch
     import torch.distributed as dist
 
-    from channel_gpu_amd.parallel.bootstrap import init_distributed, nccl_unique_id
+    from channel_gpu_amd.parallel.bootstrap import force_comm, init_distributed, nccl_unique_id
+    from channel_gpu_amd.parallel.decomposition import SlabDecomposition
     from channel_gpu_amd import require_native
     from channel_gpu_amd.utils.config import default_config
 
@@ -72,22 +115,42 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
 
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for _ in range(args.warmup):
         solver.step(False)
     barrier()
-    if args.phases:
-        solver.set_phase_timing(True)
+    solver.set_step_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         solver.step(False)
     barrier()
-    dt_wall = time.perf_counter() - t0
-    if world > 1:
-        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([dt_wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt_wall = float(t.item())
+    dt_wall = max_over_ranks(time.perf_counter() - t0)
+    step_ms = solver.step_times_ms()
+    solver.set_step_timing(False)
+    med = max_over_ranks(_pct(step_ms, 0.5))
+    p90 = max_over_ranks(_pct(step_ms, 0.9))
+    graph = bool(solver.graph_active())
     L = solver.log()
+
+    phase = None
+    if args.phases or solver.comm_kind() != "none":
+        # untimed for the headline: eager steps with per-phase events (serialised at P = 1)
+        solver.reset_phase_times()
+        solver.set_phase_timing(True)
+        ps = max(1, args.phase_steps)
+        for _ in range(ps):
+            solver.step(False)
+        solver.set_phase_timing(False)
+        barrier()
+        phase = [max_over_ranks(x / ps) for x in solver.phase_times_ms()]
+
     s_per_step = dt_wall / max(1, args.steps)
     pts = NX * NY * NZP
     value = pts / s_per_step
@@ -100,12 +163,13 @@ def main() -> None:
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * s_per_step,
+        "ms_per_step_median": med,
+        "ms_per_step_p90": p90,
         "wall_sec_per_step": s_per_step,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "reference_model_floor_s_per_step": floor,
-        "speedup_vs_reference_model_floor": (floor / s_per_step) if floor else None,
+        "reference_model_floor_s_per_step_analytic": floor,
         "dtype": "fp32 storage, fp64 y-solves" if args.precision == "fp32" else args.precision,
         "data": "synthetic (seeded random divergence-free IC on the laminar profile)",
         "config": {
@@ -115,20 +179,33 @@ def main() -> None:
             "seq_len": pts,
             "parallelism": (f"slab{world}" if solver.plan.Pr == 1
                             else f"pencil{solver.plan.Pr}x{solver.plan.Pc}"),
-            "hipgraph": not args.no_graph,
+            "hipgraph": graph,
+            "comm": solver.comm_kind(),
         },
         "health": int(L.health),
         "dt": L.dt,
     }
-    if args.phases:
-        out["phase_ms_per_step"] = [x / max(1, args.steps) for x in solver.phase_times_ms()]
+    if phase is not None:
+        out["phase_ms_per_step"] = {k: round(v, 4) for k, v in zip(PHASES, phase) if v > 0}
+        out["phase_sum_ms_compute"] = round(sum(phase[i] for i in (0, 1, 2, 3)), 4)
+        if solver.comm_kind() != "none" and solver.plan.Pr == 1:
+            esz = 16 if args.precision == "fp64" else 8
+            dec = SlabDecomposition(NX, NY, NZP // 2 + 1, world)
+            per_peer = [b for q, b in enumerate(dec.a2a_bytes_per_peer_per_step(rank, esz)) if q != rank or world == 1]
+            a2a_ms = phase[4]
+            out["a2a_ms_per_step"] = round(a2a_ms, 4)
+            out["a2a_bytes_per_peer_per_step"] = int(max(per_peer))
+            out["a2a_GBps_per_peer"] = (round(max(per_peer) / (a2a_ms * 1e-3) / 1e9, 2) if a2a_ms > 0 else None)
     if os.environ.get("CHANNEL_KSPEC_PROF"):
         # shader-clock cycles per K-SPEC phase, summed over all waves (warmup + timed steps)
         cyc = solver.kspec_profile()
         tot = sum(cyc) or 1.0
         out["kspec_phase_fraction"] = [round(c / tot, 4) for c in cyc]
+    if force_comm():
+        out["forced_comm"] = True
     if rank == 0:
         print(json.dumps(out), flush=True)
+    del solver
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

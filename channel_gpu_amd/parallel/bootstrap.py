@@ -34,13 +34,25 @@ def dist_info() -> tuple[int, int, int]:
     return rank, world, local
 
 
-def nccl_unique_id() -> bytes:
-    """Create the communicator id on rank 0 and share it with every rank (empty for 1 rank).
+def force_comm() -> bool:
+    """CHANNEL_FORCE_COMM=1: run the distributed (exchange-based) pipeline even on one rank."""
+    return os.environ.get("CHANNEL_FORCE_COMM", "0") == "1"
 
-    RCCL ncclUniqueId by default; a "shm:<name>" id when CHANNEL_COMM=shm."""
+
+def nccl_unique_id(force: bool | None = None) -> bytes:
+    """Create the communicator id on rank 0 and share it with every rank.
+
+    RCCL ncclUniqueId by default; a "shm:<name>" id when CHANNEL_COMM=shm.  One rank gets an empty
+    id (the single-rank fast path) unless ``force`` (default: CHANNEL_FORCE_COMM=1): then it gets
+    its own id and the solver builds a real 1-rank communicator and runs the P > 1 pipeline."""
     rank, world, _ = dist_info()
+    if force is None:
+        force = force_comm()
+    shm = os.environ.get("CHANNEL_COMM", "rccl").lower() == "shm"
     if world == 1:
-        return b""
+        if not force:
+            return b""
+        return f"shm:channel_{os.getpid()}_{uuid.uuid4().hex[:10]}".encode() if shm else require_native().new_unique_id()
     if not dist.is_initialized():
         raise RuntimeError("world_size > 1 requires torch.distributed to be initialised")
     if os.environ.get("CHANNEL_COMM", "rccl").lower() == "shm":
@@ -60,6 +72,15 @@ def init_distributed(backend: str | None = None) -> tuple[int, int, int]:
             backend = os.environ.get("CHANNEL_DIST_BACKEND", "gloo")
         dist.init_process_group(backend=backend)
     rank, world, local = dist_info()
+    ndev = torch.cuda.device_count()
+    shm = os.environ.get("CHANNEL_COMM", "rccl").lower() == "shm"
+    if world > 1 and ndev > 0 and not shm:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if local_world > ndev:
+            raise RuntimeError(
+                f"{local_world} ranks on this node but only {ndev} visible GPU(s): RCCL needs one GPU per rank "
+                f"(it refuses two ranks on one device: 'Duplicate GPU detected'). Use a node with >= {local_world} "
+                "GPUs, or CHANNEL_COMM=shm to rehearse the multi-rank path over the shared-memory loopback.")
     if torch.cuda.is_available():
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(local % max(1, ndev))
     return rank, world, local

@@ -52,6 +52,14 @@ class SlabDecomposition:
         ys, yc = self.y_split()
         return [yc[q] * kc[rank] * self.nkz * esz for q in range(self.P)]
 
+    def a2a_bytes_per_peer_per_step(self, rank: int, esz: int = 8) -> list[int]:
+        """bytes ``rank`` sends to each peer per RK3 step: per substep 6 backward fields (its kx
+        columns of the peer's y rows) and 3 forward fields (its y rows of the peer's kx columns);
+        the entry for ``rank`` itself is the on-device self copy."""
+        ks, kc = self.kx_split()
+        ys, yc = self.y_split()
+        return [3 * (6 * yc[q] * kc[rank] + 3 * yc[rank] * kc[q]) * self.nkz * esz for q in range(self.P)]
+
     def a2a_off_rank_bytes_per_step(self, esz: int = 8) -> int:
         """off-rank bytes per RK3 step for the busiest rank (6 backward + 3 forward per substep)."""
         worst = 0

@@ -325,8 +325,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("steps_done", &Solver::steps_done)
       .def("set_time", &Solver::set_time)
       .def("set_use_graph", &Solver::set_use_graph)
-      .def("set_phase_timing", &Solver::set_phase_timing)
+      .def("set_phase_timing", &Solver::set_phase_timing, py::call_guard<py::gil_scoped_release>())
       .def("phase_times_ms", &Solver::phase_times_ms)
+      .def("reset_phase_times", &Solver::reset_phase_times)
+      .def("set_step_timing", &Solver::set_step_timing)
+      .def("step_times_ms", &Solver::step_times_ms, py::call_guard<py::gil_scoped_release>())
+      .def("graph_active", &Solver::graph_active)
+      .def("comm_kind", &Solver::comm_kind)
       .def("kspec_profile", &Solver::kspec_profile)
       .def("symmetrize", &Solver::symmetrize)
       .def("substep_debug", &Solver::substep_debug, py::call_guard<py::gil_scoped_release>())

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
 
 #include "channel/common.hpp"
@@ -44,6 +45,7 @@ RcclComm::RcclComm(int rank, int nranks, const std::string& uid, int device) {
   ncclComm_t c;
   NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
   comm_ = c;
+  if (const char* e = std::getenv("CHANNEL_A2A_SELF")) self_via_rccl_ = std::string(e) == "rccl";
 }
 
 RcclComm::~RcclComm() {
@@ -65,13 +67,47 @@ bool RcclComm::async_error() {
 void RcclComm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
                          void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
                          hipStream_t s) {
+  A2ABlock b;
+  b.send = send;
+  b.recv = recv;
+  b.scount = scount;
+  b.soff = soff;
+  b.rcount = rcount;
+  b.roff = roff;
+  alltoallv_batch({b}, s);
+}
+
+// All blocks of the batch go out in ONE ncclGroupStart/End, so RCCL schedules the sends and
+// receives of every field to a peer over that peer's xGMI link together (one launch, every link
+// busy at once).  The self block never leaves the device: a stream-ordered D2D copy
+// (graph-capturable) unless CHANNEL_A2A_SELF=rccl.
+void RcclComm::alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) {
   auto c = static_cast<ncclComm_t>(comm_);
-  const char* sb = static_cast<const char*>(send);
-  char* rb = static_cast<char*>(recv);
+  CH_CHECK(c, "RcclComm: communicator was aborted");
+  const bool self_copy = !self_via_rccl_;
+  bool any_remote = false;
+  for (const auto& o : ops) {
+    CH_CHECK(o.scount.size() == static_cast<size_t>(size_) && o.rcount.size() == static_cast<size_t>(size_),
+             "alltoallv: count vectors must have one entry per rank");
+    if (self_copy && o.scount[rank_]) {
+      CH_CHECK(o.scount[rank_] == o.rcount[rank_], "alltoallv: self block send/recv sizes differ");
+      HIP_CHECK(hipMemcpyAsync(static_cast<char*>(o.recv) + o.roff[rank_],
+                               static_cast<const char*>(o.send) + o.soff[rank_], o.scount[rank_],
+                               hipMemcpyDeviceToDevice, s));
+    }
+    for (int p = 0; p < size_; ++p)
+      if (!(self_copy && p == rank_) && (o.scount[p] || o.rcount[p])) any_remote = true;
+  }
+  if (!any_remote) return;
   NCCL_CHECK(ncclGroupStart());
-  for (int p = 0; p < size_; ++p) {
-    if (scount[p]) NCCL_CHECK(ncclSend(sb + soff[p], scount[p] / 4, ncclFloat, p, c, s));
-    if (rcount[p]) NCCL_CHECK(ncclRecv(rb + roff[p], rcount[p] / 4, ncclFloat, p, c, s));
+  for (const auto& o : ops) {
+    const char* sb = static_cast<const char*>(o.send);
+    char* rb = static_cast<char*>(o.recv);
+    for (int p = 0; p < size_; ++p) {
+      if (self_copy && p == rank_) continue;
+      if (o.scount[p]) NCCL_CHECK(ncclSend(sb + o.soff[p], o.scount[p] / 4, ncclFloat, p, c, s));
+      if (o.rcount[p]) NCCL_CHECK(ncclRecv(rb + o.roff[p], o.rcount[p] / 4, ncclFloat, p, c, s));
+    }
   }
   NCCL_CHECK(ncclGroupEnd());
 }
@@ -177,7 +213,13 @@ void ShmComm::alltoallv(const void* send, const std::vector<size_t>& scount, con
                         void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
                         hipStream_t s) {
   HIP_CHECK(hipStreamSynchronize(s));
+  if (scount[rank_]) {  // self block: device-to-device, never through host memory
+    CH_CHECK(scount[rank_] == rcount[rank_], "alltoallv: self block send/recv sizes differ");
+    HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + roff[rank_], static_cast<const char*>(send) + soff[rank_],
+                        scount[rank_], hipMemcpyDeviceToDevice));
+  }
   for (int p = 0; p < size_; ++p) {
+    if (p == rank_) continue;
     CH_CHECK(scount[p] <= slot_bytes_ && rcount[p] <= slot_bytes_,
              "ShmComm slot too small (" << scount[p] << " bytes); set CHANNEL_SHM_SLOT_MB");
     if (scount[p])
@@ -185,7 +227,7 @@ void ShmComm::alltoallv(const void* send, const std::vector<size_t>& scount, con
   }
   barrier();
   for (int p = 0; p < size_; ++p)
-    if (rcount[p])
+    if (p != rank_ && rcount[p])
       HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + roff[p], slot(p, rank_), rcount[p], hipMemcpyHostToDevice));
   barrier();
 }

@@ -85,13 +85,17 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
   HIP_CHECK(hipSetDevice(device_));
   HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
-  if (nranks > 1) {
+  // A communicator exists for P > 1, and also at P = 1 when a unique id is passed: that runs the
+  // distributed (exchange-based) pipeline on one rank, e.g. a real 1-rank RCCL communicator on a
+  // one-GPU box, so the RCCL data plane and its graph capture are exercised on any machine.
+  if (nranks > 1 || !nccl_uid.empty()) {
     CH_CHECK(!nccl_uid.empty(), "P > 1 requires an RCCL unique id");
     comm_ = Comm::create(rank, nranks, nccl_uid, device_);
-    // Multi-rank steps run eagerly by default (~100 launches per RK3 step, negligible at these
-    // grid sizes); capturing RCCL into the step graph is opt-in (CHANNEL_GRAPH_MULTI=1).
+    // RCCL exchanges are captured into the step graph like everything else (the first step runs
+    // eagerly so RCCL sets up its peer connections outside capture); CHANNEL_GRAPH_MULTI=0 keeps
+    // multi-rank steps eager.  The host-staged ShmComm is never capturable.
     const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
-    if (!comm_->graph_capturable() || !(gm && std::atoi(gm) == 1)) use_graph_ = false;
+    if (!comm_->graph_capturable() || (gm && std::atoi(gm) == 0)) use_graph_ = false;
     if (const char* t = std::getenv("CHANNEL_COMM_TIMEOUT_S")) comm_timeout_s_ = std::atof(t);
   }
   ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
@@ -123,7 +127,7 @@ void Solver::alloc() {
   HIP_CHECK(hipMalloc(&phys_, std::max<size_t>(6 * physn_, 1) * esz_));
   HIP_CHECK(hipMemset(state_, 0, 4 * spec_ * esz_));
   HIP_CHECK(hipMemset(out_, 0, 6 * spec_ * esz_));
-  if (p.P > 1) {
+  if (comm_) {
     HIP_CHECK(hipMalloc(&xbuf_, 6 * xstride_ * esz_));
     HIP_CHECK(hipMemset(xbuf_, 0, 6 * xstride_ * esz_));
   }
@@ -159,7 +163,11 @@ void Solver::alloc() {
     ychunk_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, (144ull << 20) / plane)));
   }
   ystreams_ = 2;
-  if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = std::atoi(yc);
+  // P > 1 slab: the same byte budget per chunk; each chunk is also one batched exchange per
+  // direction, so the exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms
+  // of chunk k
+  ychunk_p_ = ychunk_;
+  if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::atoi(ys);
   std::vector<double> invdy(N);
   const auto& y = grid_.y;
@@ -179,8 +187,6 @@ void Solver::alloc() {
   HIP_CHECK(hipEventCreateWithFlags(&ev_fwd_done_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_red_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_stats_, hipEventDisableTiming));
-  ph_ev_.resize(2 * 8);
-  for (auto& e : ph_ev_) HIP_CHECK(hipEventCreate(&e));
   ph_ms_.assign(8, 0.0);
 }
 
@@ -189,7 +195,17 @@ void Solver::free_all() {
     if (gexec_[i]) (void)hipGraphExecDestroy(gexec_[i]);
   for (auto* v : {&ev_a2a_, &ev_xf_, &ev_b_, &ev_bb_})
     for (auto e : *v) (void)hipEventDestroy(e);
-  for (auto e : ph_ev_) (void)hipEventDestroy(e);
+  for (auto e : tev_pool_) (void)hipEventDestroy(e);
+  for (auto* v : {&ev_cb_, &ev_cc_})
+    for (auto e : *v) (void)hipEventDestroy(e);
+  for (auto& pr : step_ev_) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  tev_pool_.clear();
+  ev_cb_.clear();
+  ev_cc_.clear();
+  step_ev_.clear();
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
     if (e) (void)hipEventDestroy(e);
   for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_})
@@ -324,6 +340,8 @@ void Solver::set_time(double t, double dt) {
 }
 
 double Solver::time() const {
+  // the step runs on the non-blocking compute stream: wait for it before reading the device time
+  HIP_CHECK(hipStreamSynchronize(s_comp_));
   double t = 0;
   HIP_CHECK(hipMemcpy(&t, d_time_, sizeof(double), hipMemcpyDeviceToHost));
   return t;
@@ -413,22 +431,64 @@ void Solver::a2a_rows(void* xexp, void* zrows, bool to_z) {
   else comm_->alltoallv(zrows, sc, so, xexp, rc, ro, s_comm_);
 }
 
-void Solver::ev(int phase, bool end) {
+void Solver::ev(int phase, bool end, hipStream_t s) {
   // roctx ranges name the phases in rocprofv3 --marker-trace timelines (host-side, no-ops otherwise)
   static const char* kPhaseNames[8] = {"kspec", "x_backward", "z_physical", "x_forward", "a2a", "reduce", "io", "other"};
   if (end) roctxRangePop();
   else roctxRangePushA(kPhaseNames[phase & 7]);
   if (!phase_timing_) return;
-  HIP_CHECK(hipEventRecord(ph_ev_[2 * phase + (end ? 1 : 0)], s_comp_));
-  if (end) {
-    HIP_CHECK(hipEventSynchronize(ph_ev_[2 * phase + 1]));
-    float ms = 0;
-    HIP_CHECK(hipEventElapsedTime(&ms, ph_ev_[2 * phase], ph_ev_[2 * phase + 1]));
-    ph_ms_[phase] += ms;
+  hipEvent_t e = timing_event();
+  HIP_CHECK(hipEventRecord(e, s ? s : s_comp_));
+  if (!end) topen_[phase & 7] = e;
+  else tpairs_.push_back({phase & 7, topen_[phase & 7], e});
+}
+
+hipEvent_t Solver::timing_event() {
+  if (tev_used_ == tev_pool_.size()) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    tev_pool_.push_back(e);
   }
+  return tev_pool_[tev_used_++];
+}
+
+void Solver::flush_phase_events() {
+  if (!tpairs_.empty()) {
+    synchronize();
+    for (const auto& t : tpairs_) {
+      float ms = 0;
+      HIP_CHECK(hipEventElapsedTime(&ms, t.a, t.b));
+      ph_ms_[t.phase] += ms;
+    }
+  }
+  tpairs_.clear();
+  tev_used_ = 0;
+}
+
+void Solver::set_phase_timing(bool on) {
+  if (on && !phase_timing_) synchronize();
+  phase_timing_ = on;
 }
 
 std::vector<double> Solver::phase_times_ms() { return ph_ms_; }
+
+void Solver::reset_phase_times() { ph_ms_.assign(8, 0.0); }
+
+std::vector<double> Solver::step_times_ms() {
+  synchronize();
+  std::vector<double> out;
+  for (size_t i = 0; i < step_ev_used_; ++i) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, step_ev_[i].first, step_ev_[i].second));
+    out.push_back(ms);
+  }
+  step_ev_used_ = 0;
+  return out;
+}
+
+bool Solver::graph_active() const { return use_graph_ && (gexec_[0] != nullptr || gexec_[1] != nullptr); }
+
+std::string Solver::comm_kind() const { return comm_ ? comm_->kind() : "none"; }
 
 std::vector<double> Solver::kspec_profile() {
   std::vector<unsigned long long> h(kKspecPhases, 0);
@@ -487,15 +547,15 @@ void Solver::transforms(int n, bool /*stats*/) {
     dst.ndst = 1;
     dst.kx_start[0] = 0;
     dst.kx_start[1] = p.nkx;
-    // (phase timing attributes per stage, so it runs the whole-slab sequence)
-    if (ychunk_ > 0 && ychunk_ < p.ny_loc && !phase_timing_) {
+    if (ychunk_ > 0 && ychunk_ < p.ny_loc) {
       // y-chunked x -> z -> x pipeline: the physical intermediates of one chunk of y planes
       // (9 fields x chunk x NX x nkz) are produced and consumed back to back, so they are served
       // from the 256 MB Infinity Cache instead of making a full HBM round trip per stage
       // chunks alternate between the compute and the (idle at P = 1) comm stream, so one chunk's
       // launch tail overlaps the next chunk's transforms (chunks are independent; the CFL maxima
       // are atomic)
-      const bool two = ystreams_ > 1;
+      // (phase timing serialises the chunks on one stream so the stage times add up to the step)
+      const bool two = ystreams_ > 1 && !phase_timing_;
       roctxRangePushA("xzx_ychunked");
       if (two) {
         HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
@@ -512,15 +572,21 @@ void Solver::transforms(int n, bool /*stats*/) {
         XSrc sc = src;
         sc.base = static_cast<char*>(out_) + so;
         xc.nfields = 6;
+        ev(1, false, cs);
         xfft_backward(xc, sc, ph, tw_x_, fp64_, cs);
+        ev(1, true, cs);
         ZArgs zc = za;
         zc.ny = ny;
         zc.y0 = p.y0 + y0;
+        ev(2, false, cs);
         zphys(zc, ph, tw_z_, fp64_, cs);
+        ev(2, true, cs);
         XDst dc = dst;
         dc.base = static_cast<char*>(out_) + so;
         xc.nfields = 3;
+        ev(3, false, cs);
         xfft_forward(xc, ph, dc, tw_x_, fp64_, cs);
+        ev(3, true, cs);
       }
       if (two) {
         HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
@@ -543,7 +609,11 @@ void Solver::transforms(int n, bool /*stats*/) {
     ev(3, true);
     return;
   }
-  // ---- P > 1: per-field exchanges on the comm stream, overlapped with the x transforms ----
+  if (!p.pencil()) {
+    transforms_slab(n, xa, za, da);
+    return;
+  }
+  // ---- pencil: per-field exchanges on the comm stream, overlapped with the x transforms ----
   const int Pc = p.Pc, Pr = p.Pr;
   const bool pen = p.pencil();
   XSrc src;
@@ -581,7 +651,9 @@ void Solver::transforms(int n, bool /*stats*/) {
   HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
   HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
   for (int f = 0; f < 6; ++f) {
+    ev(4, false, s_comm_);
     a2a_spec(field_ptr(OUT0 + f), fld(xbuf_, xstride_, f), true);
+    ev(4, true, s_comm_);
     HIP_CHECK(hipEventRecord(ev_a2a_[f], s_comm_));
   }
   ev(1, false);
@@ -593,7 +665,9 @@ void Solver::transforms(int n, bool /*stats*/) {
     if (pen) {  // ship field f's x-blocks to the row group while field f+1 is transformed
       HIP_CHECK(hipEventRecord(ev_b_[f], s_comp_));
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_b_[f], 0));
+      ev(4, false, s_comm_);
       a2a_rows(fld(phys_, physn_, f), fld(zbuf_, zstride_, f), true);
+      ev(4, true, s_comm_);
     }
   }
   ev(1, true);
@@ -609,7 +683,9 @@ void Solver::transforms(int n, bool /*stats*/) {
   if (n == 0) {
     HIP_CHECK(hipEventRecord(ev_phys_, s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_phys_, 0));
+    ev(5, false, s_comm_);
     comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+    ev(5, true, s_comm_);
     HIP_CHECK(hipEventRecord(ev_red_, s_comm_));
     HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_red_, 0));
     dt_update(da, s_comp_);
@@ -618,7 +694,9 @@ void Solver::transforms(int n, bool /*stats*/) {
     HIP_CHECK(hipEventRecord(ev_phys_, s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_phys_, 0));
     for (int f = 0; f < 3; ++f) {
+      ev(4, false, s_comm_);
       a2a_rows(fld(phys_, physn_, f), fld(zbuf_, zstride_, f), false);
+      ev(4, true, s_comm_);
       HIP_CHECK(hipEventRecord(ev_bb_[f], s_comm_));
     }
   }
@@ -630,11 +708,143 @@ void Solver::transforms(int n, bool /*stats*/) {
     xfft_forward(xa, fld(phys_, physn_, f), df, tw_x_, fp64_, s_comp_);
     HIP_CHECK(hipEventRecord(ev_xf_[f], s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_xf_[f], 0));
+    ev(4, false, s_comm_);
     a2a_spec(field_ptr(OUT0 + f), fld(xbuf_, xstride_, f), false);
+    ev(4, true, s_comm_);
   }
   ev(3, true);
   HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
   HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+}
+
+// Exchange of y chunk k for the slab (Pr = 1): chunk k holds rows [k*ch, (k+1)*ch) of EVERY
+// rank's y range, so the chunk count is the same on all ranks (uneven splits send empty blocks
+// at the end).  Backward (to_phys): my spectral rows Y_c[k] of fields 0..nf-1 go to rank c and
+// land in c's receive block [src][y_loc][nkx_src][kz] at row k*ch; forward: the transformed rows
+// of my chunk go back into the owners' spectral rows.  Both sides are contiguous in memory, so
+// there is no pack/unpack pass (the reference ran 5 cublasCgeam passes around each host-staged
+// MPI_Alltoall, channel_cuda_mpi.c:64-128).
+void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
+  const Plan& p = plan_;
+  const int P = p.P, lines = p.lines_loc();
+  const size_t nr_me = static_cast<size_t>(std::max(0, std::min(ch, p.ny_loc - k * ch)));
+  std::vector<A2ABlock> ops(nf);
+  for (int f = 0; f < nf; ++f) {
+    A2ABlock& o = ops[f];
+    o.scount.assign(P, 0);
+    o.soff.assign(P, 0);
+    o.rcount.assign(P, 0);
+    o.roff.assign(P, 0);
+    char* spec = static_cast<char*>(field_ptr(OUT0 + f));
+    char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+    for (int c = 0; c < P; ++c) {
+      const size_t nr_c = static_cast<size_t>(std::max(0, std::min(ch, p.y_split.count[c] - k * ch)));
+      const size_t yo = (static_cast<size_t>(p.y_split.start[c]) + static_cast<size_t>(k) * ch) * lines * esz_;
+      const size_t yc = nr_c * lines * esz_;
+      const size_t xo = (static_cast<size_t>(p.ny_loc) * p.kx_split.start[c] +
+                         static_cast<size_t>(k) * ch * p.kx_split.count[c]) * p.nkz_loc * esz_;
+      const size_t xc = nr_me * p.kx_split.count[c] * p.nkz_loc * esz_;
+      if (to_phys) {
+        o.soff[c] = yc ? yo : 0;
+        o.scount[c] = yc;
+        o.roff[c] = xc ? xo : 0;
+        o.rcount[c] = xc;
+      } else {
+        o.soff[c] = xc ? xo : 0;
+        o.scount[c] = xc;
+        o.roff[c] = yc ? yo : 0;
+        o.rcount[c] = yc;
+      }
+    }
+    o.send = to_phys ? static_cast<const void*>(spec) : static_cast<const void*>(xb);
+    o.recv = to_phys ? static_cast<void*>(xb) : static_cast<void*>(spec);
+  }
+  comm_->alltoallv_batch(ops, s_comm_);
+}
+
+// P > 1 slab substep transforms, y-chunked and pipelined over two streams:
+//   comm:  B(0) B(1) F(0) B(2) F(1) ... F(nch-1) [CFL allreduce]
+//   comp:       x->z->x(0)  x->z->x(1) ...
+// B(k) = backward exchange of chunk k (6 fields, one batched group), F(k) = forward exchange of
+// chunk k (3 fields).  While chunk k is transformed, chunk k+1 arrives and chunk k-1 returns, and
+// the x-expanded intermediates of a chunk are produced and consumed back to back (served from the
+// Infinity Cache).  The arithmetic is identical to the unchunked sequence (bitwise).
+void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const DtArgs& da) {
+  const Plan& p = plan_;
+  const int P = p.P;
+  const int maxrows = p.y_split.max_count();
+  const int ch = (ychunk_p_ > 0 && ychunk_p_ < maxrows) ? ychunk_p_ : maxrows;
+  const int nch = (maxrows + ch - 1) / ch;
+  while (static_cast<int>(ev_cb_.size()) < nch) {
+    hipEvent_t a, b;
+    HIP_CHECK(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+    ev_cb_.push_back(a);
+    ev_cc_.push_back(b);
+  }
+  XArgs xa = xa0;
+  xa.nkz = p.nkz_loc;
+  xa.field_stride_spec = static_cast<long long>(xstride_);
+  XSrc src;
+  src.base = xbuf_;
+  src.nsrc = P;
+  XDst dst;
+  dst.base = xbuf_;
+  dst.ndst = P;
+  for (int c = 0; c < P; ++c) src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
+  src.kx_start[P] = dst.kx_start[P] = p.nkx;
+
+  roctxRangePushA("xzx_slab_chunked");
+  HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  auto backward = [&](int k) {
+    ev(4, false, s_comm_);
+    a2a_slab_chunk(k, ch, true, 6);
+    ev(4, true, s_comm_);
+    HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
+  };
+  backward(0);
+  for (int k = 0; k < nch; ++k) {
+    if (k + 1 < nch) backward(k + 1);
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_cb_[k], 0));
+    const int y0 = k * ch, ny = std::max(0, std::min(ch, p.ny_loc - y0));
+    if (ny > 0) {
+      for (int c = 0; c < P; ++c)
+        src.off[c] = dst.off[c] = (static_cast<long long>(p.ny_loc) * p.kx_split.start[c] +
+                                   static_cast<long long>(y0) * p.kx_split.count[c]) * p.nkz_loc;
+      XArgs xc = xa;
+      xc.ny = ny;
+      xc.nfields = 6;
+      char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz_loc * esz_;
+      ev(1, false);
+      xfft_backward(xc, src, ph, tw_x_, fp64_, s_comp_);
+      ev(1, true);
+      ZArgs zc = za0;
+      zc.ny = ny;
+      zc.y0 = p.y0 + y0;
+      ev(2, false);
+      zphys(zc, ph, tw_z_, fp64_, s_comp_);
+      ev(2, true);
+      xc.nfields = 3;
+      ev(3, false);
+      xfft_forward(xc, ph, dst, tw_x_, fp64_, s_comp_);
+      ev(3, true);
+    }
+    HIP_CHECK(hipEventRecord(ev_cc_[k], s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_cc_[k], 0));
+    ev(4, false, s_comm_);
+    a2a_slab_chunk(k, ch, false, 3);
+    ev(4, true, s_comm_);
+  }
+  if (n == 0) {  // every chunk's z stage precedes ev_cc_[nch-1], which the comm stream waited on
+    ev(5, false, s_comm_);
+    comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+    ev(5, true, s_comm_);
+  }
+  HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+  if (n == 0) dt_update(da, s_comp_);
+  roctxRangePop();
 }
 
 void Solver::prepare() {
@@ -654,11 +864,24 @@ void Solver::step(bool stats_for_next) {
   if (!prepared_) prepare();
   const int gi = stats_for_next ? 1 : 0;
   bool done = false;
-  if (use_graph_ && !debug_sync_enabled() && !phase_timing_) {
+  if (step_timing_) {
+    if (step_ev_used_ == step_ev_.size()) {
+      hipEvent_t a, b;
+      HIP_CHECK(hipEventCreate(&a));
+      HIP_CHECK(hipEventCreate(&b));
+      step_ev_.emplace_back(a, b);
+    }
+    HIP_CHECK(hipEventRecord(step_ev_[step_ev_used_].first, s_comp_));
+  }
+  // P > 1: the first step runs eagerly so RCCL connects its peers outside stream capture
+  const bool warm = !comm_ || comm_warm_;
+  if (use_graph_ && warm && !debug_sync_enabled() && !phase_timing_) {
     if (!gexec_[gi] && !graph_ok_[gi]) {
       try {
         hipGraph_t g = nullptr;
-        HIP_CHECK(hipStreamBeginCapture(s_comp_, hipStreamCaptureModeGlobal));
+        // thread-local capture with a communicator: RCCL's proxy thread keeps making HIP calls
+        const hipStreamCaptureMode mode = comm_ ? hipStreamCaptureModeThreadLocal : hipStreamCaptureModeGlobal;
+        HIP_CHECK(hipStreamBeginCapture(s_comp_, mode));
         try {
           step_body(stats_for_next);
         } catch (...) {
@@ -684,6 +907,9 @@ void Solver::step(bool stats_for_next) {
     }
   }
   if (!done) step_body(stats_for_next);
+  comm_warm_ = true;
+  if (step_timing_) HIP_CHECK(hipEventRecord(step_ev_[step_ev_used_++].second, s_comp_));
+  if (phase_timing_) flush_phase_events();
   if (stats_for_next) stats_pending_ = true;
   ++nstep_;
 }

@@ -20,17 +20,29 @@
 
 namespace channel {
 
+// one variable all-to-all of a batch (counts/offsets in bytes, per peer)
+struct A2ABlock {
+  const void* send = nullptr;
+  void* recv = nullptr;
+  std::vector<size_t> scount, soff, rcount, roff;
+};
+
 class Comm {
  public:
   virtual ~Comm() = default;
   int rank() const { return rank_; }
   int size() const { return size_; }
   virtual bool graph_capturable() const = 0;
+  virtual const char* kind() const = 0;  // "rccl" | "shm"
 
   // variable all-to-all; counts/offsets in bytes (multiples of 4)
   virtual void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
                          void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
                          hipStream_t s) = 0;
+  // several all-to-alls issued as one exchange (RCCL: one group); default: one after the other
+  virtual void alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) {
+    for (const auto& o : ops) alltoallv(o.send, o.scount, o.soff, o.recv, o.rcount, o.roff, s);
+  }
   virtual void allreduce_max_f32(float* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) = 0;
@@ -51,8 +63,10 @@ class RcclComm final : public Comm {
   RcclComm(int rank, int nranks, const std::string& uid, int device);
   ~RcclComm() override;
   bool graph_capturable() const override { return true; }
+  const char* kind() const override { return "rccl"; }
   void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
                  const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
+  void alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) override;
   void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
   void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
@@ -61,6 +75,9 @@ class RcclComm final : public Comm {
 
  private:
   void* comm_ = nullptr;  // ncclComm_t
+  // the block a rank sends to itself is a D2D copy on the stream; CHANNEL_A2A_SELF=rccl routes it
+  // through ncclSend/ncclRecv instead (lets a 1-rank communicator exercise RCCL's point-to-point path)
+  bool self_via_rccl_ = false;
 };
 
 class ShmComm final : public Comm {
@@ -68,6 +85,7 @@ class ShmComm final : public Comm {
   ShmComm(int rank, int nranks, const std::string& name);
   ~ShmComm() override;
   bool graph_capturable() const override { return false; }
+  const char* kind() const override { return "shm"; }
   void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
                  const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
   void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;

@@ -76,8 +76,21 @@ class Solver {
   long steps_done() const { return nstep_; }
   void set_time(double t, double dt);
   void set_use_graph(bool on) { use_graph_ = on; }
-  void set_phase_timing(bool on) { phase_timing_ = on; }
-  std::vector<double> phase_times_ms();  // accumulated per-phase times (phase_timing mode)
+  // true when the RK3 step is replayed from a captured hipGraph (after the first captured step)
+  bool graph_active() const;
+  // the communicator's kind ("rccl" | "shm") or "none" for the single-rank fast path
+  std::string comm_kind() const;
+  // per-phase timing: hipEvents around every stage on its own stream (no host sync inside the
+  // step; the pairs are resolved once per step).  Runs eagerly and, at P = 1, on one stream so the
+  // stages are serialised and the phase times add up to the step time.
+  void set_phase_timing(bool on);
+  // accumulated per-phase times [kspec, x_backward, z_physical, x_forward, a2a, reduce, io, other]
+  std::vector<double> phase_times_ms();
+  void reset_phase_times();
+  // per-step device times: hipEvents recorded on the compute stream around every step() (graph
+  // launches included); step_times_ms() synchronises and returns (and clears) them
+  void set_step_timing(bool on) { step_timing_ = on; }
+  std::vector<double> step_times_ms();
   // K-SPEC per-phase shader-clock sums over all waves (only with CHANNEL_KSPEC_PROF set)
   std::vector<double> kspec_profile();
   void symmetrize();                  // kz=0 Hermitian symmetry (P == 1 only)
@@ -121,7 +134,13 @@ class Solver {
   void a2a_spec(const void* spec, void* xb, bool to_phys);
   void a2a_rows(void* xexp, void* zrows, bool to_z);
   void step_body(bool stats);
-  void ev(int phase, bool end);
+  void ev(int phase, bool end, hipStream_t s = nullptr);
+  void flush_phase_events();
+  hipEvent_t timing_event();
+  // P > 1 slab: y-chunked backward exchange -> x -> z -> x -> forward exchange pipeline
+  void transforms_slab(int n, const XArgs& xa, const ZArgs& za, const DtArgs& da);
+  // exchange of y chunk k (rows [k*ch, (k+1)*ch) of every rank's y range) for nf fields
+  void a2a_slab_chunk(int k, int ch, bool to_phys, int nf);
   void write_logs(const StepLog& L, bool verbose);
   void write_stats_files(const std::vector<double>& st);
   void write_spectra_files(const Spectra& sp);
@@ -164,9 +183,23 @@ class Solver {
 
   std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
-  std::vector<hipEvent_t> ph_ev_;
+  std::vector<hipEvent_t> ev_cb_, ev_cc_;  // per y-chunk: backward exchange done, compute done
+  int ychunk_p_ = 0;                       // y planes per chunk of the P > 1 slab pipeline
+  // phase timing: event pool and the (phase, start, end) pairs of the current step
+  struct TPair {
+    int phase;
+    hipEvent_t a, b;
+  };
+  std::vector<hipEvent_t> tev_pool_;
+  size_t tev_used_ = 0;
+  std::vector<TPair> tpairs_;
+  hipEvent_t topen_[8] = {};
   std::vector<double> ph_ms_;
   bool phase_timing_ = false;
+  bool step_timing_ = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> step_ev_;
+  size_t step_ev_used_ = 0;
+  bool comm_warm_ = false;  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
 
   // rollback snapshot
   void* snap_ = nullptr;

@@ -64,8 +64,12 @@ def _assemble(parts, field):
     return out
 
 
-@pytest.mark.parametrize("world,pr", [(2, 1), (3, 1), (2, 2), (4, 2)])
-def test_multirank_matches_oracle(native, world, pr):
+@pytest.mark.parametrize("world,pr,chunk", [(2, 1, "0"), (3, 1, "0"), (3, 1, "4"), (2, 1, "1"), (2, 2, "0"),
+                                            (4, 2, "0")])
+def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk):
+    """chunk: y planes per exchange chunk of the slab pipeline (0 = whole slab; 4 with NY=33 over 3
+    ranks gives uneven ranks a different number of non-empty chunks)."""
+    monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
     nsteps = 2
     ref = ora.OracleSolver(**GRID, Re=400.0, dt_fixed=0.01)
     phi, om, U = _global_state()

@@ -86,3 +86,32 @@ def test_pencil_grid_mismatch(native):
     c = cfg(native, NX=64, NY=65, NZ=33, decomposition="pencil", pr=3)
     with pytest.raises(RuntimeError):
         native.Plan.make(c, 4, 0)
+
+
+@pytest.mark.parametrize("P,per_peer_mb", [(2, 180.0), (4, 45.0), (8, 11.2)])
+def test_a2a_per_peer_bytes_match_survey_model(P, per_peer_mb):
+    """Per-peer exchange volume of the slab pipeline vs SURVEY §5.8's truncated model at Re_tau~950
+    (1024x385x1024, fp32): one field of one transpose to one peer is (NY/P)(nkx/P)nkz x 8 B; a
+    step moves 27 such blocks (9 fields x 3 substeps) to every peer."""
+    d = SlabDecomposition(1024, 385, 513, P)
+    ys, yc = d.y_split()
+    ks, kc = d.kx_split()
+    one = [yc[q] * kc[0] * d.nkz * 8 for q in range(1, P)]  # rank 0 -> q, one field, backward
+    # SURVEY §5.8 lists 45 MB per peer at P=4 and 11.2 MB at P=8 (truncated); P=2 is 4x the P=4 block
+    assert abs(max(one) / 1e6 - per_peer_mb) / per_peer_mb < 0.03
+    per_step = d.a2a_bytes_per_peer_per_step(0)
+    for q in range(1, P):
+        assert per_step[q] == 3 * (6 * yc[q] * kc[0] + 3 * yc[0] * kc[q]) * d.nkz * 8
+        assert abs(per_step[q] / (27 * one[q - 1]) - 1) < 0.03
+
+
+def test_bench_refuses_work_skipping_env(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CHANNEL_FFT_DIAG="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "work-skipping" in (r.stderr + r.stdout)

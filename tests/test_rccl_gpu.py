@@ -1,0 +1,106 @@
+"""The distributed pipeline on a real RCCL communicator, on a one-GPU box.
+
+A 1-rank RCCL communicator (ncclCommInitRank with nranks = 1, built when the solver is given a
+unique id at P = 1) runs the P > 1 slab code path: the y-chunked batched exchanges
+(RcclComm::alltoallv_batch), the x transforms gathering from exchange blocks, the CFL
+allreduce (allreduce_max_f32), the statistics allreduce (allreduce_sum_f64), the health
+allreduce (allreduce_max_u32) and the watchdog's ncclCommGetAsyncError polling — captured into
+the step hipGraph.  Every result must be bitwise the single-rank fast path (same arithmetic, only
+the data movement differs).  CHANNEL_A2A_SELF=rccl routes the self block through ncclSend/Recv
+instead of a D2D copy, so RCCL's point-to-point path itself is exercised (and captured).
+"""
+import numpy as np
+import pytest
+
+from channel_gpu_amd.utils.config import default_config
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
+          log_every=0, symmetry_every=0)
+
+
+def _run(native, uid, nsteps=3, graph=True, stats=False, **kw):
+    cfg = default_config(**{**KW, **kw})
+    s = native.Solver(cfg, 0, 1, 0, uid)
+    s.set_use_graph(graph)
+    s.init_ic()
+    s.prepare()
+    for i in range(nsteps):
+        s.step(stats and i == nsteps - 1)
+    st = s.stats() if stats else None
+    phi, om, U = s.get_state()
+    L = s.log()
+    return s, phi, om, U, L, st
+
+
+def _same(a, b):
+    return all(np.array_equal(x, y) for x, y in zip(a[1:4], b[1:4])) and a[4].dt == b[4].dt
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_rccl_1rank_equals_fast_path(native, precision):
+    ref = _run(native, b"", precision=precision)
+    got = _run(native, native.new_unique_id(), precision=precision)
+    assert got[0].comm_kind() == "rccl" and ref[0].comm_kind() == "none"
+    assert _same(ref, got)
+    assert got[4].health == 0 and np.isfinite(got[1]).all()
+
+
+def test_rccl_graph_capture(native):
+    """RCCL exchanges inside the captured step graph: the graph is really used and bitwise eager."""
+    uid_a, uid_b = native.new_unique_id(), native.new_unique_id()
+    g = _run(native, uid_a, nsteps=4, graph=True)
+    e = _run(native, uid_b, nsteps=4, graph=False)
+    assert g[0].graph_active() and not e[0].graph_active()
+    assert _same(g, e)
+
+
+@pytest.mark.parametrize("chunk", ["1", "4", "7", "0"])
+def test_rccl_ychunks(native, monkeypatch, chunk):
+    """Chunked exchanges (ragged last chunk) are bitwise the whole-slab exchange and the fast path."""
+    ref = _run(native, b"")
+    monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
+    got = _run(native, native.new_unique_id())
+    assert _same(ref, got)
+
+
+def test_rccl_self_block_through_p2p(native, monkeypatch):
+    """CHANNEL_A2A_SELF=rccl: the self block goes through ncclSend/ncclRecv (grouped, captured)."""
+    ref = _run(native, b"")
+    monkeypatch.setenv("CHANNEL_A2A_SELF", "rccl")
+    monkeypatch.setenv("CHANNEL_YCHUNK", "9")
+    got = _run(native, native.new_unique_id(), nsteps=4)
+    assert got[0].graph_active()
+    ref4 = _run(native, b"", nsteps=4)
+    assert _same(ref4, got)
+    del ref
+
+
+def test_rccl_statistics_and_health(native):
+    """Statistics step: plane sums go through the RCCL sum allreduce, health through the max."""
+    ref = _run(native, b"", stats=True)
+    got = _run(native, native.new_unique_id(), stats=True)
+    assert np.allclose(got[5], ref[5], rtol=1e-13, atol=0) and np.abs(got[5]).max() > 0
+    assert got[0].health() == 0
+    got[0].barrier()
+
+
+def test_rccl_phase_timing(native):
+    """Per-phase events on both streams of the distributed pipeline (bench.py's exchange timing)."""
+    cfg = default_config(**KW)
+    s = native.Solver(cfg, 0, 1, 0, native.new_unique_id())
+    s.init_ic()
+    s.prepare()
+    s.step(False)
+    s.set_phase_timing(True)
+    for _ in range(2):
+        s.step(False)
+    s.set_phase_timing(False)
+    ph = s.phase_times_ms()
+    assert ph[0] > 0 and ph[1] > 0 and ph[2] > 0 and ph[3] > 0 and ph[4] > 0
+    s.set_step_timing(True)
+    for _ in range(3):
+        s.step(False)
+    t = s.step_times_ms()
+    assert len(t) == 3 and all(x > 0 for x in t)

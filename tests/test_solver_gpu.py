@@ -41,9 +41,11 @@ def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
         assert rel(gU, o.U) < 1e-11, f"U step {it}"
 
 
-@pytest.mark.parametrize("precision,NY", [("fp32", 385), ("fp32", 633), ("fp64", 633)])
+@pytest.mark.parametrize("precision,NY", [("fp32", 129), ("fp64", 129), ("fp32", 257), ("fp64", 257), ("fp32", 385),
+                                          ("fp32", 633), ("fp64", 633), ("fp32", 769)])
 def test_gpu_matches_oracle_large_ny(native, precision, NY):
-    """Tall lines: R = 7 (register prefetch slots) and R = 10 (deferred slots, LDS-staged tables)."""
+    """Tall lines: R = 3, 4 (address-only prefetch slots), R = 7 (register prefetch slots),
+    R = 10 and 13->16 (deferred slots, LDS-staged tables)."""
     NX, NZ, dt = 16, 9, 1e-4
     kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision=precision, dt_fixed=dt, stats_every=0, log_every=0,
               symmetry_every=0, ic="zero")
@@ -149,6 +151,34 @@ def test_turbulent_smoke_128(native, tmp_path):
     assert abs(L.flux - 1.8) < 0.05  # flux before the correction of the last substep
     for f in ["MEANPROFILE.dat", "UTAU.dat", "STATISTICS.dat", "URMS.dat", "RSTRSS.dat"]:
         assert (tmp_path / f).exists(), f
+
+
+def test_t_end_stops_run(native):
+    """run() stops at the first step whose end time reaches t_end (device time read after a sync)."""
+    s = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="random", stats_every=0,
+                    log_every=0, symmetry_every=0, dt_fixed=0.01, t_end=0.055)
+    s.init_ic()
+    s.run(100, False)
+    assert s.steps_done() == 6
+    assert abs(s.time() - 0.06) < 1e-12
+
+
+def test_phase_times_add_up(native):
+    """Per-phase event timing (serialised chunked pipeline) accounts for the whole step."""
+    s = make_solver(native, NX=512, NY=257, NZ=257, Re=11150.0, precision="fp32", ic="random", stats_every=0,
+                    log_every=0, symmetry_every=0)
+    s.init_ic()
+    s.prepare()
+    for _ in range(3):
+        s.step(False)
+    s.set_phase_timing(True)
+    s.set_step_timing(True)
+    for _ in range(4):
+        s.step(False)
+    steps = s.step_times_ms()
+    s.set_phase_timing(False)
+    ph = s.phase_times_ms()
+    assert sum(ph[:4]) > 0.8 * sum(steps) and sum(ph[:4]) <= 1.001 * sum(steps)
 
 
 def test_restart_roundtrip(native, tmp_path):

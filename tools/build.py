@@ -59,6 +59,29 @@ def _stale(out: str, deps: list[str], hdr_time: float) -> bool:
     return any(os.path.getmtime(d) > t for d in deps) or hdr_time > t
 
 
+def _depfile_deps(obj: str) -> list[str] | None:
+    """Headers an object was compiled against (from the compiler's -MMD file), or None."""
+    d = obj + ".d"
+    if not os.path.exists(d):
+        return None
+    text = open(d).read().replace("\\\n", " ")
+    deps = []
+    for line in text.splitlines():
+        if ":" not in line:
+            continue
+        for tok in line.split(":", 1)[1].split():
+            if tok.endswith((".hpp", ".h")) and tok.startswith(ROOT):
+                deps.append(tok)
+    return deps
+
+
+def _obj_stale(obj: str, src: str, hdr_time: float) -> bool:
+    deps = _depfile_deps(obj)
+    if deps is None:  # no dependency file yet: any newer header rebuilds
+        return _stale(obj, [src], hdr_time)
+    return _stale(obj, [src] + [h for h in deps if os.path.exists(h)], 0.0) or any(not os.path.exists(h) for h in deps)
+
+
 def _torch_flags() -> tuple[list[str], list[str]]:
     import torch.utils.cpp_extension as ce  # noqa: F401  (paths only; no JIT build)
     import torch
@@ -86,10 +109,10 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
-        if _stale(o, [s], hdr):
+        if _obj_stale(o, s, hdr):
             flags = COMMON + (DEVICE if s.endswith(".hip") else [])
             extra = ["-x", "hip"] if s.endswith(".hip") else []
-            jobs_list.append([HIPCC] + flags + extra + ["-c", s, "-o", o])
+            jobs_list.append([HIPCC] + flags + extra + ["-MMD", "-MF", o + ".d", "-c", s, "-o", o])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for f in [ex.submit(_run, c, verbose) for c in jobs_list]:
             f.result()
@@ -99,10 +122,11 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
     # bindings
     bsrc = os.path.join(ROOT, "csrc", "bindings", "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
-    if _stale(bobj, [bsrc], hdr) or _stale(EXT_SO, [bobj, CORE_SO], 0.0):
+    if _obj_stale(bobj, bsrc, hdr) or _stale(EXT_SO, [bobj, CORE_SO], 0.0):
         tcf, tld = _torch_flags()
-        if _stale(bobj, [bsrc], hdr):
-            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{INC}", *tcf, "-c", bsrc, "-o", bobj], verbose)
+        if _obj_stale(bobj, bsrc, hdr):
+            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{INC}", *tcf, "-MMD", "-MF", bobj + ".d", "-c", bsrc, "-o",
+                  bobj], verbose)
         _run([HIPCC, "-shared", "-fPIC", bobj, "-o", EXT_SO, f"-L{LIBDIR}", "-lchannel_core", *tld,
               "-Wl,-rpath,$ORIGIN/lib"], verbose)
     if driver:
