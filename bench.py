@@ -10,6 +10,10 @@ GPUs of one node with the slab decomposition (one rank per GPU, RCCL all-to-all 
 ``--gpus N > 1`` without a torchrun environment launches itself under torch.distributed.run as a
 child process (before anything touches the GPU) and exits with its return code.
 
+Ranks never import torch: the solver runs on /opt/rocm's HIP runtime and RCCL, bootstrapped by a
+native TCP rendezvous (channel_gpu_amd.parallel.native_bootstrap); torch.distributed.run is only
+the launcher.
+
 Synthetic data: a seeded random divergence-free velocity field on a laminar mean profile
 (no checkpoint is available offline).  W untimed warm-up steps (the first one eager, then graph
 capture), then exactly K RK3 steps timed between barrier + device synchronisation on every rank;
@@ -86,42 +90,34 @@ def main() -> None:
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(_self_launch(args.gpus))
 
-    import torch
-    import torch.distributed as dist
-
-    from channel_gpu_amd.parallel.bootstrap import force_comm, init_distributed, nccl_unique_id
+    # torch-free ranks: the solver runs on /opt/rocm's HIP runtime and RCCL (like the C++ driver);
+    # the native TCP rendezvous hands out the communicator id
+    os.environ["CHANNEL_TORCH_FREE"] = "1"
+    from channel_gpu_amd import require_core
     from channel_gpu_amd.parallel.decomposition import SlabDecomposition
-    from channel_gpu_amd import require_native
+    from channel_gpu_amd.parallel.native_bootstrap import init_native
     from channel_gpu_amd.utils.config import default_config
 
-    rank, world, local = init_distributed()
+    ri = init_native()
+    rank, world = ri.rank, ri.world
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    C = require_native()
+    C = require_core()
     NX, NY, NZP = (int(v) for v in args.grid.lower().split("x"))
     cfg = default_config(NX=NX, NY=NY, NZ=NZP // 2 + 1, Re=args.re, precision=args.precision, ic="random",
                          ic_amplitude=0.05, stats_every=0, log_every=0, symmetry_every=0, checkpoint_every=0,
                          health_check=True, decomposition=args.decomposition, pr=args.pr)
-    uid = nccl_unique_id()
-    solver = C.Solver(cfg, rank, world, torch.cuda.current_device(), uid)
+    solver = C.Solver(cfg, rank, world, ri.device, ri.uid)
     if args.no_graph:
         solver.set_use_graph(False)
     solver.init_ic()
     solver.prepare()
 
     def barrier():
-        solver.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
+        solver.barrier()  # device allreduce over the solver's communicator + stream sync
 
     def max_over_ranks(x: float) -> float:
-        if world == 1:
-            return x
-        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        return float(solver.max_over_ranks(float(x)))
 
     for _ in range(args.warmup):
         solver.step(False)
@@ -201,14 +197,12 @@ def main() -> None:
         cyc = solver.kspec_profile()
         tot = sum(cyc) or 1.0
         out["kspec_phase_fraction"] = [round(c / tot, 4) for c in cyc]
-    if force_comm():
+    if ri.uid and world == 1:
         out["forced_comm"] = True
     if rank == 0:
         print(json.dumps(out), flush=True)
+    barrier()
     del solver
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -3,7 +3,8 @@
 Same behaviour as the C++ binary ``bin/channel_mi355x`` (and the reference's channelMPI.bin,
 main.c:10-150), for launches through ``torchrun`` / ``torch.distributed.run`` (one rank per GPU):
 config -> device = LOCAL_RANK -> RCCL communicator -> IC (files or generated) -> RK3 loop with
-the reference stdout blocks and .dat statistics -> G/DDV/UMEAN restart files.
+the reference stdout blocks and .dat statistics -> G/DDV/UMEAN restart files.  The ranks are
+torch-free (native TCP rendezvous of the RCCL id; /opt/rocm HIP runtime and RCCL).
 """
 from __future__ import annotations
 
@@ -20,15 +21,15 @@ def main(argv=None) -> int:
     ap.add_argument("--quiet", action="store_true")
     a = ap.parse_args(argv)
 
-    import torch  # noqa: F401
+    import os
 
+    os.environ.setdefault("CHANNEL_TORCH_FREE", "1")
     from .models.channel import ChannelFlow
-    from .parallel.bootstrap import init_distributed
     from .utils.config import load_config
 
-    rank, world, _ = init_distributed()
     cfg = load_config(a.config, a.set)
     flow = ChannelFlow(cfg)
+    rank, world = flow.rank, flow.world
     flow.initialize()
     n = cfg.nsteps if a.steps is None else a.steps
     t0 = time.perf_counter()

@@ -8,21 +8,21 @@ from __future__ import annotations
 
 from typing import Iterable
 
-from .._native import require_native
+from .._native import require_core
 
 
 def load_config(path: str, overrides: Iterable[str] = ()):
     """Parse a run.conf file; ``overrides`` are ``key=value`` strings (CLI ``--set``)."""
-    return require_native().Config.from_file(path, list(overrides))
+    return require_core().Config.from_file(path, list(overrides))
 
 
 def config_from_string(text: str, overrides: Iterable[str] = ()):
-    return require_native().Config.from_string(text, list(overrides))
+    return require_core().Config.from_string(text, list(overrides))
 
 
 def default_config(**kw):
     """A Config with the reference defaults, updated from keyword arguments."""
-    c = require_native().Config()
+    c = require_core().Config()
     for k, v in kw.items():
         if not hasattr(c, k):
             raise KeyError(f"unknown config key {k!r}")

@@ -118,6 +118,9 @@ void RcclComm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
 void RcclComm::allreduce_sum_f64(double* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
+void RcclComm::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
+  NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclDouble, ncclMax, static_cast<ncclComm_t>(comm_), s));
+}
 void RcclComm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, static_cast<ncclComm_t>(comm_), s));
 }
@@ -253,6 +256,9 @@ void ShmComm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
 }
 void ShmComm::allreduce_sum_f64(double* buf, size_t n, hipStream_t s) {
   allreduce(buf, n, s, [](double a, double b) { return a + b; });
+}
+void ShmComm::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
+  allreduce(buf, n, s, [](double a, double b) { return a > b ? a : b; });
 }
 void ShmComm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
   allreduce(buf, n, s, [](unsigned a, unsigned b) { return a > b ? a : b; });

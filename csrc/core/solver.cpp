@@ -13,6 +13,10 @@
 #include <sstream>
 #include <thread>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "channel/common.hpp"
@@ -58,6 +62,28 @@ void thomas(const std::vector<double>& a, const std::vector<double>& b, const st
   for (int i = n - 2; i >= 0; --i) d[i] = dp[i] - cp[i] * d[i + 1];
 }
 }  // namespace
+
+namespace {
+void crash_handler(int sig) {
+  static const char msg[] = "\n[channel] fatal signal; native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+struct CrashTraceAtLoad {
+  CrashTraceAtLoad() {
+    const char* e = std::getenv("CHANNEL_CRASH_TRACE");
+    if (e && std::atoi(e) == 1) install_crash_handler();
+  }
+} g_crash_trace_at_load;
+}  // namespace
+
+void install_crash_handler() {
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGILL, SIGFPE}) signal(sig, crash_handler);
+}
 
 bool debug_sync_enabled() { return g_debug_sync; }
 void set_debug_sync(bool on) { g_debug_sync = on; }
@@ -136,8 +162,9 @@ void Solver::alloc() {
     HIP_CHECK(hipMemset(zbuf_, 0, 6 * zstride_ * esz_));
   }
   const int N = p.NY;
-  // scalars: dt, time, dtlog[8], stats[4N], mean[3N+8], invdy[N], maxima[4] (float), health
-  const size_t nd = 2 + 8 + 4 * N + (3 * N + 8) + N;
+  // scalars: dt, time, dtlog[8], stats[4N], mean[3N+8], invdy[N], host-reduction scratch,
+  // maxima[4] (float), health
+  const size_t nd = 2 + 8 + 4 * N + (3 * N + 8) + N + 1;
   const size_t nbytes = nd * sizeof(double) + 32 + kKspecPhases * sizeof(unsigned long long);
   HIP_CHECK(hipMalloc(&dscal_, nbytes));
   HIP_CHECK(hipMemset(dscal_, 0, nbytes));
@@ -148,7 +175,8 @@ void Solver::alloc() {
   d_stats_ = d + 10;
   d_mean_ = d_stats_ + 4 * N;
   d_invdy_ = d_mean_ + 3 * N + 8;
-  d_max_ = reinterpret_cast<float*>(d_invdy_ + N);
+  d_red_ = d_invdy_ + N;
+  d_max_ = reinterpret_cast<float*>(d_red_ + 1);
   d_health_ = reinterpret_cast<unsigned*>(d_max_ + 4);
   d_kprof_ = reinterpret_cast<unsigned long long*>(static_cast<char*>(dscal_) + nd * sizeof(double) + 32);
   kprof_on_ = std::getenv("CHANNEL_KSPEC_PROF") != nullptr;
@@ -880,7 +908,12 @@ void Solver::step(bool stats_for_next) {
       try {
         hipGraph_t g = nullptr;
         // thread-local capture with a communicator: RCCL's proxy thread keeps making HIP calls
-        const hipStreamCaptureMode mode = comm_ ? hipStreamCaptureModeThreadLocal : hipStreamCaptureModeGlobal;
+        hipStreamCaptureMode mode = comm_ ? hipStreamCaptureModeThreadLocal : hipStreamCaptureModeGlobal;
+        if (const char* m = std::getenv("CHANNEL_CAPTURE_MODE")) {
+          const std::string ms(m);
+          mode = ms == "global" ? hipStreamCaptureModeGlobal
+                                : (ms == "relaxed" ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal);
+        }
         HIP_CHECK(hipStreamBeginCapture(s_comp_, mode));
         try {
           step_body(stats_for_next);
@@ -960,6 +993,16 @@ void Solver::barrier() {
     wait(s_comm_);
   }
   synchronize();
+}
+
+double Solver::max_over_ranks(double v) {
+  if (!comm_) return v;
+  synchronize();
+  HIP_CHECK(hipMemcpy(d_red_, &v, sizeof(double), hipMemcpyHostToDevice));
+  comm_->allreduce_max_f64(d_red_, 1, s_comm_);
+  wait(s_comm_);
+  HIP_CHECK(hipMemcpy(&v, d_red_, sizeof(double), hipMemcpyDeviceToHost));
+  return v;
 }
 
 StepLog Solver::log() {

@@ -35,6 +35,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "%s\n", e.what());
     return 2;
   }
+  if (const char* ct = std::getenv("CHANNEL_CRASH_TRACE"); ct && std::atoi(ct) == 1) install_crash_handler();
   std::string conf = "run.conf";
   std::vector<std::string> overrides;
   long steps = -1;
@@ -64,7 +65,9 @@ int main(int argc, char** argv) {
       std::stringstream ss;
       ss << f.rdbuf();
       std::string uid;
-      if (pi.size > 1) {
+      // CHANNEL_FORCE_COMM=1: a communicator (and the exchange-based pipeline) even for one rank
+      const char* fc = std::getenv("CHANNEL_FORCE_COMM");
+      if (pi.size > 1 || (fc && std::atoi(fc) == 1)) {
         // CHANNEL_COMM=shm: host shared-memory loopback (ranks sharing one GPU, testing only)
         const char* cm = std::getenv("CHANNEL_COMM");
         const char* mp = std::getenv("MASTER_PORT");

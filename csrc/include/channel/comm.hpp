@@ -45,6 +45,7 @@ class Comm {
   }
   virtual void allreduce_max_f32(float* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) = 0;
+  virtual void allreduce_max_f64(double* buf, size_t n, hipStream_t s) = 0;
   virtual void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) = 0;
   virtual void abort() = 0;
   // asynchronous communicator failure (peer died, network error); polled by the solver's watchdog
@@ -69,6 +70,7 @@ class RcclComm final : public Comm {
   void alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) override;
   void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
   void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
   void abort() override;
   bool async_error() override;
@@ -90,6 +92,7 @@ class ShmComm final : public Comm {
                  const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
   void allreduce_max_f32(float* buf, size_t n, hipStream_t s) override;
   void allreduce_sum_f64(double* buf, size_t n, hipStream_t s) override;
+  void allreduce_max_f64(double* buf, size_t n, hipStream_t s) override;
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
   void abort() override { failed_ = true; }
   bool async_error() override { return failed_; }

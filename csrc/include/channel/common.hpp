@@ -29,6 +29,10 @@ struct Error : std::runtime_error {
 // that caused them (the reference's kernelCheck ran cudaGetLastError without a sync, check.cu:7).
 bool debug_sync_enabled();
 void set_debug_sync(bool on);
+// SIGSEGV/SIGBUS/SIGABRT handler that writes the native backtrace (execinfo) to stderr before the
+// process dies (failure diagnosis on boxes without a debugger); CHANNEL_CRASH_TRACE=1 installs it
+// at library load
+void install_crash_handler();
 
 // Number of blocks of `kernel` (with `threads` per block and `dyn_lds` dynamic LDS) that are
 // resident on the current device at once: CUs x occupancy.  Persistent kernels size their grid

@@ -125,6 +125,8 @@ class Solver {
   void transforms_debug(bool dt_update);  // backward + phys + forward only (tests)
   Comm* comm() { return comm_.get(); }
   void barrier();
+  // host value reduced (max) over all ranks through the solver's communicator (timing, control)
+  double max_over_ranks(double v);
 
  private:
   void alloc();
@@ -180,6 +182,7 @@ class Solver {
   int ystreams_ = 1;               // streams the y chunks alternate over
   int ychunk_ = 0;                 // y planes per x->z->x pipeline chunk (P = 1), 0 = whole slab
   double* d_invdy_ = nullptr;
+  double* d_red_ = nullptr;  // one double for max_over_ranks
 
   std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;

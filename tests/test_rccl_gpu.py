@@ -7,7 +7,8 @@ allreduce (allreduce_max_f32), the statistics allreduce (allreduce_sum_f64), the
 allreduce (allreduce_max_u32) and the watchdog's ncclCommGetAsyncError polling — captured into
 the step hipGraph.  Every result must be bitwise the single-rank fast path (same arithmetic, only
 the data movement differs).  CHANNEL_A2A_SELF=rccl routes the self block through ncclSend/Recv
-instead of a D2D copy, so RCCL's point-to-point path itself is exercised (and captured).
+instead of a D2D copy, so RCCL's point-to-point path itself is exercised (and captured) — in a
+torch-free process on ROCm's RCCL, the stack bench.py and the drivers run on.
 """
 import numpy as np
 import pytest
@@ -65,16 +66,41 @@ def test_rccl_ychunks(native, monkeypatch, chunk):
     assert _same(ref, got)
 
 
-def test_rccl_self_block_through_p2p(native, monkeypatch):
-    """CHANNEL_A2A_SELF=rccl: the self block goes through ncclSend/ncclRecv (grouped, captured)."""
-    ref = _run(native, b"")
-    monkeypatch.setenv("CHANNEL_A2A_SELF", "rccl")
-    monkeypatch.setenv("CHANNEL_YCHUNK", "9")
-    got = _run(native, native.new_unique_id(), nsteps=4)
-    assert got[0].graph_active()
-    ref4 = _run(native, b"", nsteps=4)
-    assert _same(ref4, got)
-    del ref
+SELF_P2P_SCRIPT = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["CHANNEL_ROOT"])
+from channel_gpu_amd import require_core
+from channel_gpu_amd.utils.config import default_config
+C = require_core()
+kw = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
+          log_every=0, symmetry_every=0)
+out = []
+for uid in (b"", C.new_unique_id()):
+    s = C.Solver(default_config(**kw), 0, 1, 0, uid)
+    s.init_ic(); s.prepare()
+    for _ in range(4):
+        s.step(False)
+    out.append((s.get_state(), s.graph_active(), s.comm_kind()))
+(a, ga, ka), (b, gb, kb) = out
+assert ka == "none" and kb == "rccl" and gb, (ka, kb, gb)
+assert all(np.array_equal(x, y) for x, y in zip(a, b))
+print("SELF_P2P_OK", flush=True)
+"""
+
+
+def test_rccl_self_block_through_p2p(native):
+    """CHANNEL_A2A_SELF=rccl: the self block goes through grouped ncclSend/ncclRecv, captured in the
+    step graph, bitwise the fast path.  Runs in a torch-free process (ROCm's RCCL, like bench.py and
+    the drivers): torch's bundled RCCL 2.26 crashes capturing a 1-rank self send/recv."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CHANNEL_TORCH_FREE="1", CHANNEL_A2A_SELF="rccl", CHANNEL_YCHUNK="9", CHANNEL_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", SELF_P2P_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "SELF_P2P_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
 
 
 def test_rccl_statistics_and_health(native):

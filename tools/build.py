@@ -3,7 +3,8 @@
 
 Products
   channel_gpu_amd/lib/libchannel_core.so   HIP kernels + C++ core (solver, RCCL comm, HDF5 I/O, config)
-  channel_gpu_amd/_C<EXT_SUFFIX>           pybind11/PyTorch bindings
+  channel_gpu_amd/_core<EXT_SUFFIX>        torch-free pybind11 bindings (Solver, config, I/O, bootstrap)
+  channel_gpu_amd/_C<EXT_SUFFIX>           PyTorch tensor entry points of every kernel (+ re-exports _core)
   bin/channel_mi355x                       C++ driver binary (run.conf, MPI bootstrap of RCCL)
 
 Incremental: an object is rebuilt when its source or any header under csrc/include is newer.
@@ -28,6 +29,7 @@ OBJ = os.path.join(ROOT, "build", "obj")
 LIBDIR = os.path.join(ROOT, "channel_gpu_amd", "lib")
 CORE_SO = os.path.join(LIBDIR, "libchannel_core.so")
 EXT_SO = os.path.join(ROOT, "channel_gpu_amd", "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+CORE_EXT_SO = os.path.join(ROOT, "channel_gpu_amd", "_core" + sysconfig.get_config_var("EXT_SUFFIX"))
 DRIVER = os.path.join(ROOT, "bin", "channel_mi355x")
 INC = os.path.join(ROOT, "csrc", "include")
 CONDA = "/opt/conda"
@@ -110,7 +112,7 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if _obj_stale(o, s, hdr):
-            flags = COMMON + (DEVICE if s.endswith(".hip") else [])
+            flags = COMMON + DEVICE  # host .cpp too: hipcc compiles it as HIP; gfx950 code objects only
             extra = ["-x", "hip"] if s.endswith(".hip") else []
             jobs_list.append([HIPCC] + flags + extra + ["-MMD", "-MF", o + ".d", "-c", s, "-o", o])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
@@ -119,13 +121,26 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
     if _stale(CORE_SO, objs, 0.0):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", CORE_SO, "-L/opt/rocm/lib", "-lrccl",
               "-lrocprofiler-sdk-roctx", "-ldl", "-Wl,-rpath,/opt/rocm/lib", "-Wl,-soname,libchannel_core.so"], verbose)
-    # bindings
+    # torch-free bindings: pybind11 headers of the torch wheel (one pybind11 type registry shared
+    # with _C), no libtorch
+    import torch
+
+    tinc = os.path.join(os.path.dirname(torch.__file__), "include")
+    csrc_ = os.path.join(ROOT, "csrc", "bindings", "core_module.cpp")
+    cobj = os.path.join(OBJ, "core_module.o")
+    if _obj_stale(cobj, csrc_, hdr) or _stale(CORE_EXT_SO, [cobj, CORE_SO], 0.0):
+        if _obj_stale(cobj, csrc_, hdr):
+            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", *DEVICE, f"-I{INC}", f"-I{tinc}", f"-I{sysconfig.get_paths()['include']}",
+                  "-MMD", "-MF", cobj + ".d", "-c", csrc_, "-o", cobj], verbose)
+        _run([HIPCC, "-shared", "-fPIC", cobj, "-o", CORE_EXT_SO, f"-L{LIBDIR}", "-lchannel_core",
+              "-Wl,-rpath,$ORIGIN/lib"], verbose)
+    # torch bindings
     bsrc = os.path.join(ROOT, "csrc", "bindings", "bindings.cpp")
     bobj = os.path.join(OBJ, "bindings.o")
     if _obj_stale(bobj, bsrc, hdr) or _stale(EXT_SO, [bobj, CORE_SO], 0.0):
         tcf, tld = _torch_flags()
         if _obj_stale(bobj, bsrc, hdr):
-            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", f"-I{INC}", *tcf, "-MMD", "-MF", bobj + ".d", "-c", bsrc, "-o",
+            _run([HIPCC, "-O2", "-std=c++17", "-fPIC", *DEVICE, f"-I{INC}", *tcf, "-MMD", "-MF", bobj + ".d", "-c", bsrc, "-o",
                   bobj], verbose)
         _run([HIPCC, "-shared", "-fPIC", bobj, "-o", EXT_SO, f"-L{LIBDIR}", "-lchannel_core", *tld,
               "-Wl,-rpath,$ORIGIN/lib"], verbose)
@@ -134,7 +149,7 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
         dsrc = os.path.join(ROOT, "csrc", "driver", "main.cpp")
         os.makedirs(os.path.dirname(DRIVER), exist_ok=True)
         if _stale(DRIVER, [dsrc, CORE_SO], hdr):
-            _run([HIPCC, "-O2", "-std=c++17", f"-I{INC}", dsrc, "-o", DRIVER, f"-L{LIBDIR}", "-lchannel_core",
+            _run([HIPCC, "-O2", "-std=c++17", *DEVICE, f"-I{INC}", dsrc, "-o", DRIVER, f"-L{LIBDIR}", "-lchannel_core",
                   "-Wl,-rpath,$ORIGIN/../channel_gpu_amd/lib", "-Wl,-rpath,/opt/rocm/lib"], verbose)
 
 
@@ -145,7 +160,7 @@ def main() -> None:
     ap.add_argument("--no-driver", action="store_true")
     a = ap.parse_args()
     build(a.verbose, a.jobs, driver=not a.no_driver)
-    print("built:", os.path.relpath(CORE_SO, ROOT), os.path.relpath(EXT_SO, ROOT))
+    print("built:", os.path.relpath(CORE_SO, ROOT), os.path.relpath(CORE_EXT_SO, ROOT), os.path.relpath(EXT_SO, ROOT))
 
 
 if __name__ == "__main__":

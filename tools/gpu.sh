@@ -4,7 +4,7 @@
 #   bash tools/gpu.sh TAG STEP [STEP ...]
 #
 # Steps (run in order; each under its own time limit; the script stops at the first failure):
-#   tests            full GPU test suite          (PYTEST_ARGS adds selectors, e.g. "-k rccl")
+#   tests            full GPU test suite          (PYTEST_K="not slow" selects by -k, PYTEST_ARGS adds files)
 #   smoke            __graft_entry__.smoke()
 #   bench            bench.py $BENCH_ARGS         (default: the headline grid)
 #   prof             rocprofv3 --kernel-trace --stats of a short bench.py $BENCH_ARGS
@@ -28,8 +28,8 @@ for step in "$@"; do
   log=gpurun_out/${tag}_${step}.log
   case $step in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread $PYTEST_ARGS \
-        > $log 2>&1 || fail tests $log
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread \
+        ${PYTEST_K:+-k "$PYTEST_K"} $PYTEST_ARGS > $log 2>&1 || fail tests $log
       tail -n 2 $log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 || fail smoke $log
