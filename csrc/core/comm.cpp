@@ -45,6 +45,7 @@ RcclComm::RcclComm(int rank, int nranks, const std::string& uid, int device) {
   ncclComm_t c;
   NCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
   comm_ = c;
+  // (the solver normally never hands the self block to the exchange; see CHANNEL_A2A_SELF there)
   if (const char* e = std::getenv("CHANNEL_A2A_SELF")) self_via_rccl_ = std::string(e) == "rccl";
 }
 

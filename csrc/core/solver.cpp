@@ -196,6 +196,9 @@ void Solver::alloc() {
   // of chunk k
   ychunk_p_ = ychunk_;
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
+  // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
+  // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
+  if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
   if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::atoi(ys);
   std::vector<double> invdy(N);
   const auto& y = grid_.y;
@@ -766,6 +769,7 @@ void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
     char* spec = static_cast<char*>(field_ptr(OUT0 + f));
     char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
     for (int c = 0; c < P; ++c) {
+      if (self_direct_ && c == p.rank) continue;  // read/written in place by the x transforms
       const size_t nr_c = static_cast<size_t>(std::max(0, std::min(ch, p.y_split.count[c] - k * ch)));
       const size_t yo = (static_cast<size_t>(p.y_split.start[c]) + static_cast<size_t>(k) * ch) * lines * esz_;
       const size_t yc = nr_c * lines * esz_;
@@ -821,6 +825,13 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   dst.ndst = P;
   for (int c = 0; c < P; ++c) src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
   src.kx_start[P] = dst.kx_start[P] = p.nkx;
+  if (self_direct_) {  // own kx block: straight from / into the spectral fields
+    src.self_seg = dst.self_seg = p.rank;
+    src.self_base = out_;
+    dst.self_base = out_;
+    src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
+    CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
+  }
 
   roctxRangePushA("xzx_slab_chunked");
   HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
@@ -840,6 +851,8 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
       for (int c = 0; c < P; ++c)
         src.off[c] = dst.off[c] = (static_cast<long long>(p.ny_loc) * p.kx_split.start[c] +
                                    static_cast<long long>(y0) * p.kx_split.count[c]) * p.nkz_loc;
+      if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields
+        src.off[p.rank] = dst.off[p.rank] = (static_cast<long long>(p.y0) + y0) * p.lines_loc();
       XArgs xc = xa;
       xc.ny = ny;
       xc.nfields = 6;

@@ -188,6 +188,7 @@ class Solver {
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
   std::vector<hipEvent_t> ev_cb_, ev_cc_;  // per y-chunk: backward exchange done, compute done
   int ychunk_p_ = 0;                       // y planes per chunk of the P > 1 slab pipeline
+  bool self_direct_ = true;                // slab: own kx block read/written in place (no self copy)
   // phase timing: event pool and the (phase, start, end) pairs of the current step
   struct TPair {
     int phase;

@@ -94,13 +94,14 @@ struct SegPos {
   int start;      // first index of the segment
   int count;      // its length
   long long off;  // element offset of its block
+  int idx;        // segment index
 };
 template <int MAXS = 8>
 __device__ __forceinline__ SegPos seg_find(const int* start, const long long* off, int n, int i) {
-  SegPos p{start[0], start[1] - start[0], off[0]};
+  SegPos p{start[0], start[1] - start[0], off[0], 0};
 #pragma unroll
   for (int q = 1; q < MAXS; ++q)
-    if (q < n && i >= start[q]) p = SegPos{start[q], start[q + 1] - start[q], off[q]};
+    if (q < n && i >= start[q]) p = SegPos{start[q], start[q + 1] - start[q], off[q], q};
   return p;
 }
 
@@ -133,6 +134,8 @@ __global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
     const int y = rest % a.ny, f = rest / a.ny;
     const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
+    // this rank's own block is read in place from its spectral field (no self exchange)
+    const T2* sbase = src.self_seg >= 0 ? static_cast<const T2*>(src.self_base) + f * src.self_field_stride : base;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -141,8 +144,9 @@ __global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
       const int i = min(e / C, a.nkx - 1);
       const int kz = min(kz0 + e % C, a.nkz - 1);
       const SegPos sp = seg_find(src.kx_start, src.off, src.nsrc, i);
+      const T2* b = sp.idx == src.self_seg ? sbase : base;
       // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
-      v[q] = base[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
+      v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
     }
   };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
@@ -246,13 +250,16 @@ __global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    // this rank's own block goes straight into its spectral field (no self exchange)
+    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
     for (int e = tid; e < a.nkx * C; e += NT) {
       const int i = e / C, c = e - i * C;
       const int kz = kz0 + c;
       if (kz < a.nkz) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
         const SegPos sp = seg_find(dst.kx_start, dst.off, dst.ndst, i);
-        outb[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        T2* ob = sp.idx == dst.self_seg ? soutb : outb;
+        ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
       }
     }
   }

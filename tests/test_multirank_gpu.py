@@ -64,12 +64,16 @@ def _assemble(parts, field):
     return out
 
 
-@pytest.mark.parametrize("world,pr,chunk", [(2, 1, "0"), (3, 1, "0"), (3, 1, "4"), (2, 1, "1"), (2, 2, "0"),
-                                            (4, 2, "0")])
-def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk):
+@pytest.mark.parametrize("world,pr,chunk,self_mode", [(2, 1, "0", "direct"), (3, 1, "0", "direct"),
+                                                      (3, 1, "4", "direct"), (2, 1, "1", "direct"),
+                                                      (3, 1, "4", "copy"), (2, 2, "0", "direct"),
+                                                      (4, 2, "0", "direct")])
+def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mode):
     """chunk: y planes per exchange chunk of the slab pipeline (0 = whole slab; 4 with NY=33 over 3
-    ranks gives uneven ranks a different number of non-empty chunks)."""
+    ranks gives uneven ranks a different number of non-empty chunks); self_mode: own block in place
+    (direct) or copied inside the exchange (copy)."""
     monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
+    monkeypatch.setenv("CHANNEL_A2A_SELF", self_mode)
     nsteps = 2
     ref = ora.OracleSolver(**GRID, Re=400.0, dt_fixed=0.01)
     phi, om, U = _global_state()

@@ -57,11 +57,14 @@ def test_rccl_graph_capture(native):
     assert _same(g, e)
 
 
-@pytest.mark.parametrize("chunk", ["1", "4", "7", "0"])
-def test_rccl_ychunks(native, monkeypatch, chunk):
-    """Chunked exchanges (ragged last chunk) are bitwise the whole-slab exchange and the fast path."""
+@pytest.mark.parametrize("chunk,self_mode", [("1", "direct"), ("4", "direct"), ("7", "direct"), ("0", "direct"),
+                                             ("4", "copy"), ("0", "copy")])
+def test_rccl_ychunks(native, monkeypatch, chunk, self_mode):
+    """Chunked exchanges (ragged last chunk) are bitwise the whole-slab exchange and the fast path,
+    with the own block accessed in place (direct) or copied inside the exchange (copy)."""
     ref = _run(native, b"")
     monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
+    monkeypatch.setenv("CHANNEL_A2A_SELF", self_mode)
     got = _run(native, native.new_unique_id())
     assert _same(ref, got)
 
