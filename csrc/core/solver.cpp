@@ -554,6 +554,7 @@ void Solver::transforms(int n, bool /*stats*/) {
   da.dt = d_dt_;
   da.time = d_time_;
   da.dt_log = d_dtlog_;
+  da.health = cfg_.health_check ? d_health_ : nullptr;
   da.cfl = cfg_.cfl;
   da.dt_max = cfg_.dt_max;
   da.dt_fixed = cfg_.dt_fixed;

@@ -145,6 +145,7 @@ struct DtArgs {
   double* dt = nullptr;      // output dt (device)
   double* time = nullptr;    // accumulated time (device)
   double* dt_log = nullptr;  // [8]: umax vmax wmax cflsum dt_c dt_v dt ...
+  unsigned* health = nullptr;  // bit 1 set on non-finite CFL maxima or dt collapse
   double cfl = 0.5, dt_max = 0.05, dt_fixed = 0.0;
   int parity = 0;
   double NX = 0, NZ = 0, LX = 0, LZ = 0, Re = 0, dy_uniform = 0;

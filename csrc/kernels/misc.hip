@@ -28,6 +28,10 @@ __global__ void dt_update_kernel(DtArgs a) {
   }
   double dt = fmin(fmin(dt_c, dt_v), a.dt_max);
   if (a.dt_fixed > 0.0) dt = a.dt_fixed;
+  // health bit 1: the CFL inputs are not finite or dt collapsed (a blow-up that stays finite in the
+  // fields can still overflow the fp32 maxima and freeze the run at dt = 0)
+  if (a.health && (!isfinite(csum) || !isfinite(umax) || !isfinite(vmax) || !isfinite(wmax) || !(dt > 1e-12)))
+    atomicOr(a.health, 2u);
   *a.dt = dt;
   *a.time += dt;
   if (a.dt_log) {
