@@ -71,7 +71,7 @@ PYBIND11_MODULE(_core, m) {
       RW(NX) RW(NY) RW(NZ) RW(in_G) RW(in_DDV) RW(in_UMEAN) RW(out_G) RW(out_DDV) RW(out_UMEAN) RW(path) RW(Re) RW(Q)
       RW(LX) RW(LZ) RW(stretch) RW(nsteps) RW(t_end) RW(cfl) RW(dt_fixed) RW(dt_max) RW(cfl_mode) RW(stats_every)
       RW(symmetry_every) RW(checkpoint_every) RW(log_every) RW(precision) RW(decomposition) RW(pr) RW(pc) RW(seed)
-      RW(ic) RW(ic_amplitude) RW(forcing) RW(health_check) RW(health_every) RW(on_nan) RW(snapshot_every)
+      RW(ic) RW(ic_amplitude) RW(forcing) RW(influence) RW(explicit_d2) RW(checkpoint_async) RW(health_check) RW(health_every) RW(on_nan) RW(snapshot_every)
       RW(max_rollbacks) RW(rollback_cfl_factor) RW(spectra_every) RW(spectra_planes) RW(log_json);
 #undef RW
 
@@ -125,7 +125,8 @@ PYBIND11_MODULE(_core, m) {
   m.def("hdf5_available", &hdf5_available);
   m.def("set_debug_sync", &set_debug_sync);
   m.def("install_crash_handler", &install_crash_handler, "native backtrace on fatal signals (stderr)");
-  m.def("h5_create_field", &h5_create_field);
+  m.def("h5_create_field", &h5_create_field, py::arg("path"), py::arg("NX"), py::arg("NY"), py::arg("NZ"),
+        py::arg("fp64") = false, py::arg("Kx") = -1);
   m.def("h5_write_planes", &h5_write_planes);
   m.def("h5_read_planes", [](const std::string& p, const std::vector<int>& planes) {
     std::vector<double> d;
@@ -134,6 +135,12 @@ PYBIND11_MODULE(_core, m) {
     return std::make_pair(vec(d), std::vector<int>(dims, dims + 3));
   });
   m.def("h5_write_attrs", &h5_write_attrs);
+  m.def("h5_write_vector", &h5_write_vector);
+  m.def("h5_read_vector", [](const std::string& p, const std::string& name) {
+    std::vector<double> v;
+    const bool ok = h5_read_vector(p, name, v);
+    return py::make_tuple(ok, vec(v));
+  });
   m.def("h5_read_attrs", &h5_read_attrs);
   m.def("umean_write", &umean_write);
   m.def("umean_read", &umean_read);
@@ -198,6 +205,8 @@ PYBIND11_MODULE(_core, m) {
       .def("transforms_debug", &Solver::transforms_debug, py::call_guard<py::gil_scoped_release>())
       .def("write_restart", &Solver::write_restart, py::call_guard<py::gil_scoped_release>())
       .def("read_restart", &Solver::read_restart, py::call_guard<py::gil_scoped_release>())
+      .def("checkpoint_async", &Solver::checkpoint_async, py::call_guard<py::gil_scoped_release>())
+      .def("wait_checkpoint", &Solver::wait_checkpoint, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &Solver::barrier, py::call_guard<py::gil_scoped_release>())
       .def("max_over_ranks", &Solver::max_over_ranks, py::call_guard<py::gil_scoped_release>())
       .def("take_snapshot", &Solver::take_snapshot, py::call_guard<py::gil_scoped_release>())

@@ -201,6 +201,7 @@ Config Config::from_tree(const ConfigTree& t) {
   c.stats_every = static_cast<int>(t.get_int(pick(t, "stats_every"), c.stats_every));
   c.symmetry_every = static_cast<int>(t.get_int(pick(t, "symmetry_every"), c.symmetry_every));
   c.checkpoint_every = static_cast<int>(t.get_int(pick(t, "checkpoint_every"), c.checkpoint_every));
+  c.checkpoint_async = t.get_bool(pick(t, "checkpoint_async"), c.checkpoint_async);
   c.log_every = static_cast<int>(t.get_int(pick(t, "log_every"), c.log_every));
   c.precision = t.get_string(pick(t, "precision"), c.precision);
   c.decomposition = t.get_string(pick(t, "decomposition"), c.decomposition);
@@ -210,6 +211,8 @@ Config Config::from_tree(const ConfigTree& t) {
   c.ic = t.get_string(pick(t, "ic"), c.ic);
   c.ic_amplitude = t.get_double(pick(t, "ic_amplitude"), c.ic_amplitude);
   c.forcing = t.get_string(pick(t, "forcing"), c.forcing);
+  c.influence = t.get_string(pick(t, "influence"), c.influence);
+  c.explicit_d2 = t.get_string(pick(t, "explicit_d2"), c.explicit_d2);
   c.health_check = t.get_bool(pick(t, "health_check"), c.health_check);
   c.health_every = static_cast<int>(t.get_int(pick(t, "health_every"), c.health_every));
   c.on_nan = t.get_string(pick(t, "on_nan"), c.on_nan);
@@ -268,6 +271,8 @@ void Config::validate() const {
   CH_CHECK(decomposition == "slab" || decomposition == "pencil", "decomposition must be slab|pencil");
   CH_CHECK(cfl_mode == "corrected" || cfl_mode == "parity", "cfl_mode must be corrected|parity");
   CH_CHECK(forcing == "implicit" || forcing == "parity", "forcing must be implicit|parity");
+  CH_CHECK(influence == "discrete" || influence == "analytic", "influence must be discrete|analytic");
+  CH_CHECK(explicit_d2 == "compact" || explicit_d2 == "dd", "explicit_d2 must be compact|dd");
   CH_CHECK(ic == "random" || ic == "laminar" || ic == "file" || ic == "os_mode" || ic == "zero",
            "ic must be random|laminar|file|os_mode|zero");
   CH_CHECK(stats_every >= 0 && symmetry_every >= 0 && checkpoint_every >= 0 && log_every >= 0 &&
@@ -293,11 +298,13 @@ std::string Config::to_string() const {
   o << "  cfl = " << cfl << ";\n  dt_fixed = " << dt_fixed << ";\n  dt_max = " << dt_max << ";\n";
   o << "  cfl_mode = \"" << cfl_mode << "\";\n";
   o << "  stats_every = " << stats_every << ";\n  symmetry_every = " << symmetry_every << ";\n";
-  o << "  checkpoint_every = " << checkpoint_every << ";\n  log_every = " << log_every << ";\n";
+  o << "  checkpoint_every = " << checkpoint_every << ";\n  checkpoint_async = "
+    << (checkpoint_async ? "true" : "false") << ";\n  log_every = " << log_every << ";\n";
   o << "  precision = \"" << precision << "\";\n  decomposition = \"" << decomposition << "\";\n";
   o << "  pr = " << pr << ";\n  pc = " << pc << ";\n  seed = " << seed << ";\n";
   o << "  ic = \"" << ic << "\";\n  ic_amplitude = " << ic_amplitude << ";\n";
   o << "  forcing = \"" << forcing << "\";\n  health_check = " << (health_check ? "true" : "false") << ";\n";
+  o << "  influence = \"" << influence << "\";\n  explicit_d2 = \"" << explicit_d2 << "\";\n";
   o << "  health_every = " << health_every << ";\n  on_nan = \"" << on_nan << "\";\n";
   o << "  snapshot_every = " << snapshot_every << ";\n  max_rollbacks = " << max_rollbacks << ";\n";
   o << "  rollback_cfl_factor = " << rollback_cfl_factor << ";\n  spectra_every = " << spectra_every << ";\n";

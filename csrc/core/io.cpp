@@ -124,7 +124,7 @@ struct Hid {
 
 bool hdf5_available() { return h5raw().lib != nullptr; }
 
-void h5_create_field(const std::string& path, int NX, int NY, int NZ, bool fp64) {
+void h5_create_field(const std::string& path, int NX, int NY, int NZ, bool fp64, int Kx) {
   H5& h = h5();
   Hid f(h.Fcreate(path.c_str(), ACC_TRUNC, P_DEFAULT, P_DEFAULT), h.Fclose, "create " + path);
   const hsize_t dims[3] = {static_cast<hsize_t>(NX), static_cast<hsize_t>(NY), static_cast<hsize_t>(2 * NZ)};
@@ -134,9 +134,11 @@ void h5_create_field(const std::string& path, int NX, int NY, int NZ, bool fp64)
   h.Pset_fill_value(pl.id, *h.T_NATIVE_DOUBLE, &zero);
   Hid d(h.Dcreate2(f.id, "u", fp64 ? *h.T_NATIVE_DOUBLE : *h.T_NATIVE_FLOAT, sp.id, P_DEFAULT, pl.id, P_DEFAULT),
         h.Dclose, "create dataset u");
-  // explicitly write zero planes so the file is fully defined even without fill-value support
+  // explicitly write the zero planes nobody else writes (all of them when Kx < 0)
   std::vector<float> zp(static_cast<size_t>(NY) * 2 * NZ, 0.0f);
   for (int i = 0; i < NX; ++i) {
+    const int kx = i < NX / 2 ? i : i - NX;  // FFT order
+    if (Kx >= 0 && kx >= -Kx && kx <= Kx) continue;
     const hsize_t start[3] = {static_cast<hsize_t>(i), 0, 0};
     const hsize_t count[3] = {1, static_cast<hsize_t>(NY), static_cast<hsize_t>(2 * NZ)};
     Hid fs(h.Dget_space(d.id), h.Sclose, "filespace");
@@ -216,6 +218,32 @@ std::map<std::string, double> h5_read_attrs(const std::string& path) {
     if (h.Aread(a.id, *h.T_NATIVE_DOUBLE, &v) >= 0) out[k] = v;
   }
   return out;
+}
+
+void h5_write_vector(const std::string& path, const std::string& name, const std::vector<double>& v) {
+  H5& h = h5();
+  Hid f(h.Fopen(path.c_str(), ACC_RDWR, P_DEFAULT), h.Fclose, "open " + path);
+  const hsize_t dims[1] = {static_cast<hsize_t>(v.size())};
+  Hid sp(h.Screate_simple(1, dims, nullptr), h.Sclose, "dataspace");
+  Hid d(h.Dcreate2(f.id, name.c_str(), *h.T_NATIVE_DOUBLE, sp.id, P_DEFAULT, P_DEFAULT, P_DEFAULT), h.Dclose,
+        "create dataset " + name);
+  CH_CHECK(h.Dwrite(d.id, *h.T_NATIVE_DOUBLE, S_ALL, S_ALL, P_DEFAULT, v.data()) >= 0, "HDF5 write " << name);
+}
+
+bool h5_read_vector(const std::string& path, const std::string& name, std::vector<double>& v) {
+  H5& h = h5();
+  Hid f(h.Fopen(path.c_str(), ACC_RDONLY, P_DEFAULT), h.Fclose, "open " + path);
+  const hid_t did = h.Dopen2(f.id, name.c_str(), P_DEFAULT);
+  if (did < 0) return false;
+  Hid d(did, h.Dclose, "open dataset " + name);
+  hsize_t dims[1] = {0};
+  {
+    Hid fs(h.Dget_space(d.id), h.Sclose, "filespace");
+    CH_CHECK(h.Sget_simple_extent_dims(fs.id, dims, nullptr) == 1, "dataset " << name << " is not 1-D");
+  }
+  v.assign(dims[0], 0.0);
+  CH_CHECK(h.Dread(d.id, *h.T_NATIVE_DOUBLE, S_ALL, S_ALL, P_DEFAULT, v.data()) >= 0, "HDF5 read " << name);
+  return true;
 }
 
 void umean_write(const std::string& path, const std::vector<double>& U) {

@@ -9,6 +9,7 @@
 #include <iostream>
 #include <map>
 #include <chrono>
+#include <functional>
 #include <mutex>
 #include <sstream>
 #include <thread>
@@ -132,6 +133,11 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
 
 Solver::~Solver() {
   try {
+    wait_checkpoint();
+  } catch (const std::exception& e) {
+    std::cerr << "[channel] background checkpoint failed: " << e.what() << "\n";
+  }
+  try {
     if (s_comp_) (void)hipStreamSynchronize(s_comp_);
     if (s_comm_) (void)hipStreamSynchronize(s_comm_);
   } catch (...) {
@@ -239,9 +245,9 @@ void Solver::free_all() {
   step_ev_.clear();
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
     if (e) (void)hipEventDestroy(e);
-  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_})
+  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_})
     if (p) (void)hipFree(p);
-  state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = nullptr;
+  state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = d_sym_ = nullptr;
 }
 
 void* Solver::field_ptr(int f) const {
@@ -1075,10 +1081,56 @@ std::vector<double> Solver::mean_profile() {
 }
 
 void Solver::symmetrize() {
-  CH_CHECK(!comm_, "symmetrize: only for P == 1 (P > 1 relies on the per-substep C2R projection)");
   const Plan& p = plan_;
-  symmetrize_kz0(field_ptr(PHI), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
-  symmetrize_kz0(field_ptr(OMEGA), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+  if (!comm_) {
+    symmetrize_kz0(field_ptr(PHI), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+    symmetrize_kz0(field_ptr(OMEGA), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+    prepared_ = false;
+    return;
+  }
+  // distributed: the kz = 0 column lives on the ranks of process row 0 (slab: every rank)
+  const bool has_kz0 = p.kz0 == 0;
+  const size_t loc = static_cast<size_t>(p.NY) * p.nkx_loc, all = static_cast<size_t>(p.NY) * p.nkx;
+  if (!d_sym_) HIP_CHECK(hipMalloc(&d_sym_, 2 * (loc + all) * esz_));
+  char* col_loc = static_cast<char*>(d_sym_);
+  char* col_all = col_loc + 2 * loc * esz_;
+  std::vector<A2ABlock> ops(2);
+  for (int f = 0; f < 2; ++f) {
+    A2ABlock& o = ops[f];
+    o.scount.assign(p.P, 0);
+    o.soff.assign(p.P, 0);
+    o.rcount.assign(p.P, 0);
+    o.roff.assign(p.P, 0);
+    o.send = col_loc + f * loc * esz_;
+    o.recv = col_all + f * all * esz_;
+    if (has_kz0) {
+      for (int c = 0; c < p.Pc; ++c) {
+        const int g = p.rank_of(p.prow, c);
+        o.scount[g] = loc * esz_;
+        o.rcount[g] = static_cast<size_t>(p.NY) * p.kx_split.count[c] * esz_;
+        o.roff[g] = static_cast<size_t>(p.NY) * p.kx_split.start[c] * esz_;
+      }
+    }
+    if (has_kz0)
+      kz0_pack(field_ptr(f == 0 ? PHI : OMEGA), col_loc + f * loc * esz_, p.NY, p.nkx_loc, p.nkz_loc, fp64_, s_comp_);
+  }
+  HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
+  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_stats_, 0));
+  comm_->alltoallv_batch(ops, s_comm_);
+  HIP_CHECK(hipEventRecord(ev_stats_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_stats_, 0));
+  if (has_kz0) {
+    Kz0SymArgs a;
+    a.N = p.NY;
+    a.nkx_loc = p.nkx_loc;
+    a.nkz_loc = p.nkz_loc;
+    a.kx0 = p.kx0;
+    a.nkx = p.nkx;
+    a.nblk = p.Pc;
+    for (int c = 0; c <= p.Pc; ++c) a.kx_start[c] = c < p.Pc ? p.kx_split.start[c] : p.nkx;
+    for (int f = 0; f < 2; ++f)
+      kz0_symmetrize_dist(field_ptr(f == 0 ? PHI : OMEGA), col_all + f * all * esz_, a, fp64_, s_comp_);
+  }
   prepared_ = false;
 }
 
@@ -1201,17 +1253,20 @@ void Solver::run(long nsteps, bool verbose) {
       }
     }
     if (pe > 0 && nstep_ % pe == 0) write_spectra_files(spectra());
-    if (ye > 0 && nstep_ % ye == 0 && !comm_) {
+    if (ye > 0 && nstep_ % ye == 0) {
       symmetrize();
       prepare();
     }
     if (ce > 0 && nstep_ % ce == 0 && cfg_.out_G != "-") {
       const std::string sfx = "." + std::to_string(nstep_);
-      write_restart(cfg_.out_G + sfx, cfg_.out_DDV + sfx, cfg_.out_UMEAN != "-" ? cfg_.out_UMEAN + sfx : "-");
+      const std::string um = cfg_.out_UMEAN != "-" ? cfg_.out_UMEAN + sfx : "-";
+      if (cfg_.checkpoint_async) checkpoint_async(cfg_.out_G + sfx, cfg_.out_DDV + sfx, um);
+      else write_restart(cfg_.out_G + sfx, cfg_.out_DDV + sfx, um);
     }
     if (cfg_.t_end > 0 && time() >= cfg_.t_end) break;
   }
   synchronize();
+  wait_checkpoint();
 }
 
 // ---- failure handling ------------------------------------------------------------------------------
@@ -1371,59 +1426,151 @@ void Solver::write_json(const StepLog& L, double ms_per_step) {
 }
 
 // ---- restart I/O (Appendix B) --------------------------------------------------------------------
-void Solver::write_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
+// A restart is taken in two parts: capture (synchronous: device state -> host copy, at a step
+// boundary) and write (HDF5 planes of this rank into the one shared file, the ranks taking turns).
+// write_restart does both now; checkpoint_async hands the write to a background thread (the time
+// stepping continues) and the ranks pass the file between them through marker files, so the
+// background writers never touch the communicator.  The reference wrote only at the end, gathering
+// every plane on rank 0 with an MPI_Barrier per plane (hit_mpi.c:257-339, main.c:139-144).
+Solver::RestartJob Solver::capture_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
+  RestartJob j;
+  j.g = g;
+  j.ddv = ddv;
+  j.umean = umean;
+  j.phi.resize(spec_);
+  j.om.resize(spec_);
+  j.U.resize(plan_.NY);
+  get_state(j.phi.data(), j.om.data(), j.U.data());
+  double hv[2];
+  HIP_CHECK(hipMemcpy(hv, d_dt_, sizeof(hv), hipMemcpyDeviceToHost));
+  j.dt = hv[0];
+  j.time = hv[1];
+  j.step = nstep_;
+  j.serial = ++ckpt_serial_;
+  return j;
+}
+
+void Solver::write_restart_job(const RestartJob& j, const std::function<void(int)>& turn) {
   const Plan& p = plan_;
   const int N = p.NY, NZ = p.NZ, lines = p.lines_loc();
   const double N2 = static_cast<double>(p.NX) * p.Nzp;
-  std::vector<std::complex<double>> phi(spec_), om(spec_);
-  std::vector<double> U(N);
-  get_state(phi.data(), om.data(), U.data());
-  double hv[2];
-  HIP_CHECK(hipMemcpy(hv, d_dt_, sizeof(hv), hipMemcpyDeviceToHost));
   std::vector<int> planes(p.nkx_loc);
   for (int i = 0; i < p.nkx_loc; ++i) planes[i] = p.kx_fft_pos(p.kx0 + i);
-  // pencil ranks own a kz range of each plane: read-modify-write (ranks take turns below)
+  // pencil ranks own a kz range of each plane: read-modify-write (ranks take turns)
   auto pack = [&](const std::vector<std::complex<double>>& f, std::vector<double>& d) {
     for (int i = 0; i < p.nkx_loc; ++i)
       for (int kzl = 0; kzl < p.nkz_loc; ++kzl)
-        for (int j = 0; j < N; ++j) {
-          const auto v = f[static_cast<size_t>(j) * lines + i * p.nkz_loc + kzl] * N2;
-          const size_t o = ((static_cast<size_t>(i) * NZ + p.kz0 + kzl) * N + j) * 2;
+        for (int jy = 0; jy < N; ++jy) {
+          const auto v = f[static_cast<size_t>(jy) * lines + i * p.nkz_loc + kzl] * N2;
+          const size_t o = ((static_cast<size_t>(i) * NZ + p.kz0 + kzl) * N + jy) * 2;
           d[o] = v.real();
           d[o + 1] = v.imag();
         }
   };
-  std::map<std::string, double> attrs = {{"time", hv[1]}, {"dt", hv[0]}, {"step", static_cast<double>(nstep_)},
+  std::map<std::string, double> attrs = {{"time", j.time}, {"dt", j.dt}, {"step", static_cast<double>(j.step)},
                                          {"Re", cfg_.Re},  {"Q", cfg_.Q},   {"LX", cfg_.LX},
                                          {"LZ", cfg_.LZ},  {"NX", double(p.NX)}, {"NY", double(N)},
-                                         {"NZ", double(NZ)}, {"format_version", 1.0}};
+                                         {"NZ", double(NZ)}, {"format_version", 2.0},
+                                         {"fp64", fp64_ ? 1.0 : 0.0}};
+  int stage = 0;
   for (int which = 0; which < 2; ++which) {
-    const std::string& path = which == 0 ? g : ddv;
+    const std::string& path = which == 0 ? j.g : j.ddv;
     if (path.empty() || path == "-") continue;
-    if (p.rank == 0) {
-      h5_create_field(path, p.NX, N, NZ, false);
-      h5_write_attrs(path, attrs);
-    }
     for (int r = 0; r < p.P; ++r) {
-      barrier();
-      if (r == p.rank) {
-        std::vector<double> data(static_cast<size_t>(p.nkx_loc) * NZ * N * 2, 0.0);
-        if (p.pencil()) {
-          int dims[3];
-          h5_read_planes(path, planes, data, dims);
+      turn(stage * p.P + r);
+      if (r != p.rank) continue;
+      if (r == 0) {
+        // fp64 storage writes H5T_NATIVE_DOUBLE (the reference's unused double writers,
+        // hit_mpi.c:92-255); fp32 keeps the reference's float dataset
+        h5_create_field(path, p.NX, N, NZ, fp64_, p.Kx);
+        h5_write_attrs(path, attrs);
+        // U(y) in full precision next to "u" (the UMEAN file keeps the reference's float32 records)
+        if (which == 0 && p.owns_mean()) {
+          std::vector<double> u(N);
+          for (int jy = 0; jy < N; ++jy) u[jy] = j.U[jy] * N2;
+          h5_write_vector(path, "umean", u);
         }
-        pack(which == 0 ? om : phi, data);
-        h5_write_planes(path, planes, data);
       }
+      std::vector<double> data(static_cast<size_t>(p.nkx_loc) * NZ * N * 2, 0.0);
+      if (p.pencil()) {
+        int dims[3];
+        h5_read_planes(path, planes, data, dims);
+      }
+      pack(which == 0 ? j.om : j.phi, data);
+      h5_write_planes(path, planes, data);
     }
-    barrier();
+    ++stage;
   }
-  if (p.owns_mean() && !umean.empty() && umean != "-") {
+  turn(stage * p.P);  // everybody done
+  if (p.owns_mean() && !j.umean.empty() && j.umean != "-") {
     std::vector<double> u(N);
-    for (int j = 0; j < N; ++j) u[j] = U[j] * N2;
-    umean_write(umean, u);
+    for (int jy = 0; jy < N; ++jy) u[jy] = j.U[jy] * N2;
+    umean_write(j.umean, u);
   }
+}
+
+void Solver::write_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
+  wait_checkpoint();
+  const RestartJob j = capture_restart(g, ddv, umean);
+  // synchronous: the ranks take turns at device barriers
+  write_restart_job(j, [this](int) { barrier(); });
   barrier();
+}
+
+void Solver::checkpoint_async(const std::string& g, const std::string& ddv, const std::string& umean) {
+  wait_checkpoint();
+  RestartJob j = capture_restart(g, ddv, umean);
+  const int P = plan_.P, rank = plan_.rank;
+  const double timeout = comm_timeout_s_ > 0 ? comm_timeout_s_ : 3600.0;
+  ckpt_thread_ = std::thread([this, j = std::move(j), P, rank, timeout]() {
+    try {
+      // turn t belongs to rank t % P: rank r waits for the marker "<g>.turn" holding
+      // "<serial> <t>" written by the previous writer (atomic rename), then passes it on
+      const std::string marker = (j.g != "-" ? j.g : j.ddv) + ".turn";
+      auto wait_turn = [&](int t) {
+        if (P == 1 || t == 0) return;
+        const std::string want = std::to_string(j.serial) + " " + std::to_string(t);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (true) {
+          std::ifstream f(marker);
+          std::string line;
+          if (f.good() && std::getline(f, line) && line == want) return;
+          CH_CHECK(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < timeout,
+                   "checkpoint: rank " << rank << " timed out waiting for its turn (" << want << ")");
+          std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        }
+      };
+      auto pass_turn = [&](int t) {
+        if (P == 1) return;
+        const std::string tmp = marker + "." + std::to_string(rank);
+        {
+          std::ofstream f(tmp, std::ios::trunc);
+          f << j.serial << " " << t << "\n";
+        }
+        CH_CHECK(std::rename(tmp.c_str(), marker.c_str()) == 0, "checkpoint: cannot update " << marker);
+      };
+      // write step t belongs to rank t % P; turn(t) is called by every rank for every t in order,
+      // so a rank's write at turn `last` is complete when it sees the next turn index
+      int last = -1;
+      write_restart_job(j, [&](int t) {
+        if (last >= 0 && last % P == rank) pass_turn(last + 1);
+        if (t % P == rank) wait_turn(t);  // rank 0's final turn waits until every rank has written
+        last = t;
+      });
+      if (P > 1 && rank == 0) std::remove(marker.c_str());
+    } catch (...) {
+      ckpt_error_ = std::current_exception();
+    }
+  });
+}
+
+void Solver::wait_checkpoint() {
+  if (ckpt_thread_.joinable()) ckpt_thread_.join();
+  if (ckpt_error_) {
+    std::exception_ptr e = ckpt_error_;
+    ckpt_error_ = nullptr;
+    std::rethrow_exception(e);
+  }
 }
 
 void Solver::read_restart(const std::string& g, const std::string& ddv, const std::string& umean) {
@@ -1449,7 +1596,11 @@ void Solver::read_restart(const std::string& g, const std::string& ddv, const st
   unpack(g, om);
   unpack(ddv, phi);
   std::vector<double> U(N, 0.0);
-  if (!umean.empty() && umean != "-") {
+  std::vector<double> u64;
+  if (h5_read_vector(g, "umean", u64) && static_cast<int>(u64.size()) == N) {
+    // written by this framework: U at full precision (preferred over the float32 UMEAN file)
+    for (int jy = 0; jy < N; ++jy) U[jy] = u64[jy] / N2;
+  } else if (!umean.empty() && umean != "-") {
     U = umean_read(umean, N);
     for (auto& u : U) u /= N2;
   } else {

@@ -59,6 +59,7 @@ struct Config {
   int stats_every = 10;         // FREC_STATS (channel.h:82)
   int symmetry_every = 1000;    // RK3.c:174
   int checkpoint_every = 0;     // 0 = only at the end (reference behaviour)
+  bool checkpoint_async = true; // periodic checkpoints written by a background thread from a host copy
   int log_every = 1;            // stdout blocks / mean .dat files cadence (reference: every step)
   std::string precision = "fp32";      // storage: fp32 | fp64; y-solves are always fp64
   std::string decomposition = "slab";  // slab | pencil
@@ -67,6 +68,12 @@ struct Config {
   std::string ic = "random";    // random | laminar | file | os_mode
   double ic_amplitude = 0.1;
   std::string forcing = "implicit";    // implicit (exact flux) | parity (meanUevol.c:201-221)
+  // Reference-parity switches: wall-BC influence functions discrete (default: v'(+-1)
+  // = 0 to round-off) | analytic (the reference's cosh/sinh Green's functions, bilplacSolver_double
+  // .cu:56-250, l1/l2 typo fixed); explicit viscous D2: compact (default) | dd (D1 o D1 as in
+  // RK3_kernels.cu:160-164 / derivatives_nu_double.cu:440-446)
+  std::string influence = "discrete";
+  std::string explicit_d2 = "compact";
   bool health_check = true;
   // Failure handling (the reference only exit(1)'d the failing rank, check.cu).
   int health_every = 100;              // steps between global NaN/Inf checks

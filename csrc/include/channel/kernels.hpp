@@ -154,6 +154,15 @@ void dt_update(const DtArgs& a, hipStream_t s);
 
 // kz=0 plane Hermitian symmetrisation of a [y][nkx][nkz] field held entirely by one rank
 void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStream_t s);
+// distributed version: pack the local kz=0 column [y][kx_loc], exchange, symmetrise from the
+// gathered columns (blocks [c][y][nkx_c] of the ranks of this process row)
+struct Kz0SymArgs {
+  int N = 0, nkx_loc = 0, nkz_loc = 0, kx0 = 0, nkx = 0;
+  int nblk = 1;
+  int kx_start[9] = {0};
+};
+void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp64, hipStream_t s);
+void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool fp64, hipStream_t s);
 
 // ---- diagnostics ---------------------------------------------------------------------------
 struct SpectraArgs {

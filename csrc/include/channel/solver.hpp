@@ -14,7 +14,10 @@
 #include <hip/hip_runtime.h>
 
 #include <complex>
+#include <exception>
+#include <functional>
 #include <memory>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -93,7 +96,7 @@ class Solver {
   std::vector<double> step_times_ms();
   // K-SPEC per-phase shader-clock sums over all waves (only with CHANNEL_KSPEC_PROF set)
   std::vector<double> kspec_profile();
-  void symmetrize();                  // kz=0 Hermitian symmetry (P == 1 only)
+  void symmetrize();                  // kz=0 Hermitian symmetry (any P; one column exchange)
 
   // ---- failure handling -------------------------------------------------------
   void take_snapshot();               // device copy of (phi, omega+U, dt, time, step)
@@ -115,6 +118,10 @@ class Solver {
   // ---- restart files (reference-compatible, Appendix B) --------------------------------
   void write_restart(const std::string& g, const std::string& ddv, const std::string& umean);
   void read_restart(const std::string& g, const std::string& ddv, const std::string& umean);
+  // capture the state now (host copy) and write the files from a background thread; the next
+  // checkpoint / wait_checkpoint() / run() end / destructor joins it (and rethrows its error)
+  void checkpoint_async(const std::string& g, const std::string& ddv, const std::string& umean);
+  void wait_checkpoint();
 
   // ---- raw device access (tests / bindings) ----------------------------------------------
   enum Field { PHI = 0, OMEGA, RPHI, ROMEGA, OUT0, OUT1, OUT2, OUT3, OUT4, OUT5 };
@@ -149,6 +156,17 @@ class Solver {
   void write_json(const StepLog& L, double ms_per_step);
   void wait(hipStream_t s);           // stream sync with the communicator watchdog (P > 1)
   void invalidate_graphs();
+  struct RestartJob {
+    std::string g, ddv, umean;
+    std::vector<std::complex<double>> phi, om;
+    std::vector<double> U;
+    double time = 0, dt = 0;
+    long step = 0;
+    long serial = 0;
+  };
+  RestartJob capture_restart(const std::string& g, const std::string& ddv, const std::string& umean);
+  // turn(t) is called before every rank-ordered write step t (t % P = the writing rank)
+  void write_restart_job(const RestartJob& j, const std::function<void(int)>& turn);
 
   Config cfg_;
   Plan plan_;
@@ -203,7 +221,10 @@ class Solver {
   bool step_timing_ = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> step_ev_;
   size_t step_ev_used_ = 0;
-  bool comm_warm_ = false;  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
+  bool comm_warm_ = false;
+  std::thread ckpt_thread_;
+  std::exception_ptr ckpt_error_;
+  long ckpt_serial_ = 0;  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
 
   // rollback snapshot
   void* snap_ = nullptr;
@@ -211,6 +232,7 @@ class Solver {
   int rollbacks_ = 0;
   // spectra accumulators [ekx | ekz | map] and plane list (device)
   void* d_spec_ = nullptr;
+  void* d_sym_ = nullptr;    // kz = 0 columns (local + gathered) for the distributed symmetrisation
   size_t spec_n_ = 0;
   double comm_timeout_s_ = 900.0;     // CHANNEL_COMM_TIMEOUT_S (0 = wait forever)
 

@@ -80,6 +80,59 @@ void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStre
   HIP_LAUNCH_CHECK(s);
 }
 
+// Distributed kz = 0 symmetrisation (any P, slab or pencil): the kx lines are spread over the ranks
+// of a process row, so every rank first publishes its kz = 0 column [y][kx_loc] (pack), the
+// columns are exchanged (the solver's all-to-all; each rank receives every block of its row), and
+// each rank replaces its lines by 0.5 (q(kx) + conj q(-kx)) from the pre-symmetrisation copy, so
+// the two owners of a +-kx pair write conjugate values without further communication.  The
+// reference re-imposed the symmetry with a full backward+forward FFT round trip of both fields
+// through the global transposes (imposeSymetry.c:5-18).
+template <typename T2>
+__global__ void kz0_pack_kernel(const T2* q, T2* col, int N, int nkx_loc, int nkz_loc) {
+  const int y = blockIdx.x;
+  for (int i = threadIdx.x; i < nkx_loc; i += blockDim.x)
+    col[static_cast<size_t>(y) * nkx_loc + i] = q[(static_cast<size_t>(y) * nkx_loc + i) * nkz_loc];
+}
+
+template <typename T2>
+__global__ void kz0_sym_dist_kernel(T2* q, const T2* col, Kz0SymArgs a) {
+  const int y = blockIdx.x;
+  for (int i = threadIdx.x; i < a.nkx_loc; i += blockDim.x) {
+    const int ig = a.kx0 + i;
+    const int igp = ig == 0 ? 0 : a.nkx - ig;  // index of -kx
+    int c = 0;
+    for (int r = 1; r < a.nblk; ++r)
+      if (igp >= a.kx_start[r]) c = r;
+    const int cnt = a.kx_start[c + 1] - a.kx_start[c];
+    const T2 vp = col[static_cast<size_t>(a.N) * a.kx_start[c] + static_cast<size_t>(y) * cnt + (igp - a.kx_start[c])];
+    T2* dst = q + (static_cast<size_t>(y) * a.nkx_loc + i) * a.nkz_loc;
+    const T2 v = *dst;
+    *dst = T2{static_cast<decltype(v.x)>(0.5 * (v.x + vp.x)), static_cast<decltype(v.x)>(0.5 * (v.y - vp.y))};
+  }
+}
+
+void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp64, hipStream_t s) {
+  if (fp64)
+    hipLaunchKernelGGL(kz0_pack_kernel<double2>, dim3(N), dim3(128), 0, s, static_cast<const double2*>(q),
+                       static_cast<double2*>(col), N, nkx_loc, nkz_loc);
+  else
+    hipLaunchKernelGGL(kz0_pack_kernel<float2>, dim3(N), dim3(128), 0, s, static_cast<const float2*>(q),
+                       static_cast<float2*>(col), N, nkx_loc, nkz_loc);
+  HIP_LAUNCH_CHECK(s);
+}
+
+void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool fp64, hipStream_t s) {
+  CH_CHECK(a.nblk >= 1 && a.nblk <= 8 && a.kx_start[0] == 0 && a.kx_start[a.nblk] == a.nkx,
+           "kz0 symmetrisation: bad kx block table");
+  if (fp64)
+    hipLaunchKernelGGL(kz0_sym_dist_kernel<double2>, dim3(a.N), dim3(128), 0, s, static_cast<double2*>(q),
+                       static_cast<const double2*>(col_all), a);
+  else
+    hipLaunchKernelGGL(kz0_sym_dist_kernel<float2>, dim3(a.N), dim3(128), 0, s, static_cast<float2*>(q),
+                       static_cast<const float2*>(col_all), a);
+  HIP_LAUNCH_CHECK(s);
+}
+
 // Energy spectra of u, v, w at selected y planes (the reference's calcSpectra, statistics.cu:245-326,
 // is dead code that dumped |q|^2 of one plane; here it is a live, device-side diagnostic).
 // One block per (local kx, plane); fluctuations only (the (0,0) line carries U(y)).  The kz = 0

@@ -72,3 +72,36 @@ def test_garbage_checkpoint_raises(h5, tmp_path):
     path.write_bytes(b"not an hdf5 file" * 64)
     with pytest.raises(RuntimeError):
         h5.h5_read_planes(str(path), [0])
+
+
+def test_h5_fp64_dataset_roundtrip_exact(h5, tmp_path):
+    """fp64 storage writes an H5T_NATIVE_DOUBLE dataset (hit_mpi.c:92-255 convention): bit-exact."""
+    NX, NY, NZ = 16, 9, 5
+    path = str(tmp_path / "G64.h5")
+    h5.h5_create_field(path, NX, NY, NZ, True)
+    rng = np.random.default_rng(1)
+    data = rng.standard_normal(2 * NY * 2 * NZ)
+    h5.h5_write_planes(path, [2, 7], list(data))
+    got, dims = h5.h5_read_planes(path, [2, 7])
+    assert np.array_equal(np.asarray(got), data)
+
+
+def test_h5_create_writes_only_dealiased_planes(h5, tmp_path):
+    """With Kx given, only the dealiased planes (|kx| > Kx) are zero-written at creation; unwritten
+    retained planes still read as the zero fill value."""
+    NX, NY, NZ, Kx = 32, 9, 5, 10
+    path = str(tmp_path / "G.h5")
+    h5.h5_create_field(path, NX, NY, NZ, False, Kx)
+    z, dims = h5.h5_read_planes(path, list(range(NX)))
+    assert dims == [NX, NY, 2 * NZ] and not np.any(np.asarray(z))
+
+
+def test_h5_vector_dataset(h5, tmp_path):
+    path = str(tmp_path / "G.h5")
+    h5.h5_create_field(path, 8, 5, 3, False)
+    v = np.linspace(0.1, 1.7, 5) / 3.0
+    h5.h5_write_vector(path, "umean", list(v))
+    ok, got = h5.h5_read_vector(path, "umean")
+    assert ok and np.array_equal(np.asarray(got), v)
+    ok2, _ = h5.h5_read_vector(path, "nothere")
+    assert not ok2

@@ -47,10 +47,14 @@ def _worker(rank, world, shm, outdir, nsteps, pr=1):
     for _ in range(nsteps):
         s.step(False)
     gphi, gom, gU = s.get_state()
-    np.savez(os.path.join(outdir, f"r{rank}.npz"), phi=gphi, om=gom, U=gU, health=s.health(), kx0=p.kx0,
-             kz0=p.kz0)
     if C.hdf5_available():
         s.write_restart(os.path.join(outdir, "G.h5"), os.path.join(outdir, "DDV.h5"), os.path.join(outdir, "U.bin"))
+        s.checkpoint_async(os.path.join(outdir, "Ga.h5"), os.path.join(outdir, "DDVa.h5"), "-")
+        s.wait_checkpoint()
+    s.symmetrize()  # distributed kz=0 column exchange
+    sphi, som, _ = s.get_state()
+    np.savez(os.path.join(outdir, f"r{rank}.npz"), phi=gphi, om=gom, U=gU, sphi=sphi, som=som, health=s.health(),
+             kx0=p.kx0, kz0=p.kz0)
     del s
 
 
@@ -91,6 +95,14 @@ def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mo
         assert np.abs(gphi - ref.phi).max() < 1e-9 * np.abs(ref.phi).max()
         assert np.abs(gom - ref.om).max() < 1e-9 * np.abs(ref.om).max()
         assert np.abs(parts[0]["U"] - ref.U).max() < 1e-11
+        # distributed symmetrisation: 0.5 (q(kx) + conj q(-kx)) on the kz = 0 plane
+        for f, sf in (("phi", "sphi"), ("om", "som")):
+            g, sg = _assemble(parts, f), _assemble(parts, sf)
+            nkx = g.shape[1]
+            want = g.copy()
+            neg = (-np.arange(nkx)) % nkx
+            want[:, :, 0] = 0.5 * (g[:, :, 0] + np.conj(g[:, neg, 0]))
+            assert np.allclose(sg, want, rtol=0, atol=1e-15 * np.abs(g).max())
         if native.hdf5_available():
             from channel_gpu_amd.utils.config import default_config
 
@@ -98,6 +110,13 @@ def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mo
             s1 = native.Solver(cfg, 0, 1, 0, b"")
             s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), os.path.join(d, "U.bin"))
             rphi, rom, rU = s1.get_state()
-            # files hold float32 (reference format)
-            assert np.abs(rphi - ref.phi).max() < 1e-5 * np.abs(ref.phi).max()
-            assert np.abs(rU - ref.U).max() < 1e-5
+            gphi, gom = _assemble(parts, "phi"), _assemble(parts, "om")
+            # fp64 storage writes float64 datasets and U at full precision: exact
+            assert np.array_equal(rphi, gphi) and np.array_equal(rom, gom)
+            assert np.abs(rU - ref.U).max() < 1e-11
+            # the background writer (ranks passing the file by marker files) wrote the same data
+            s2 = native.Solver(cfg, 0, 1, 0, b"")
+            s2.read_restart(os.path.join(d, "Ga.h5"), os.path.join(d, "DDVa.h5"), "-")
+            aphi, aom, _ = s2.get_state()
+            assert np.array_equal(aphi, rphi) and np.array_equal(aom, rom)
+            assert not any(f.endswith(".turn") for f in os.listdir(d))

@@ -197,3 +197,79 @@ def test_restart_roundtrip(native, tmp_path):
     pb, ob, ub = b.get_state()
     assert rel(pb, pa) < 1e-6 and rel(ob, oa) < 1e-6 and rel(ub, ua) < 1e-6
     assert abs(b.time() - a.time()) < 1e-12
+
+
+def test_restart_fp64_resume_is_bitwise(native, tmp_path):
+    """fp64 storage writes float64 datasets (+ U at full precision): resuming from the files is
+    bitwise the continuous run (dt and time restored; zeta_0 = 0 needs no R)."""
+    if not native.hdf5_available():
+        pytest.skip("libhdf5 unavailable")
+    kw = dict(NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
+              log_every=0, symmetry_every=0)
+    a = make_solver(native, **kw)
+    a.init_ic()
+    a.prepare()
+    for _ in range(3):
+        a.step(False)
+    g, d, u = str(tmp_path / "G.h5"), str(tmp_path / "DDV.h5"), str(tmp_path / "U.bin")
+    a.write_restart(g, d, u)
+    b = make_solver(native, **kw)
+    b.read_restart(g, d, u)
+    b.prepare()
+    pa, oa, ua = a.get_state()
+    pb, ob, ub = b.get_state()
+    assert np.array_equal(pa, pb) and np.array_equal(oa, ob) and np.array_equal(ua, ub)
+    for s in (a, b):
+        for _ in range(3):
+            s.step(False)
+    pa, oa, ua = a.get_state()
+    pb, ob, ub = b.get_state()
+    assert np.array_equal(pa, pb) and np.array_equal(oa, ob) and np.array_equal(ua, ub)
+    assert a.time() == b.time()
+
+
+def test_async_checkpoints(native, tmp_path):
+    """checkpoint_every with checkpoint_async: files written by a background thread from a host copy
+    taken at the step boundary, while stepping continues; every checkpoint reads back exactly."""
+    if not native.hdf5_available():
+        pytest.skip("libhdf5 unavailable")
+    out = str(tmp_path) + "/"
+    s = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="random", ic_amplitude=0.2,
+                    stats_every=0, log_every=0, symmetry_every=0, checkpoint_every=2, checkpoint_async=True,
+                    out_G=out + "G.h5", out_DDV=out + "DDV.h5", out_UMEAN=out + "U.bin", path=out)
+    s.init_ic()
+    s.run(4, False)
+    p4, o4, u4 = s.get_state()
+    import os
+
+    assert all(os.path.exists(out + f) for f in ["G.h5.2", "DDV.h5.2", "G.h5.4", "DDV.h5.4", "U.bin.4"])
+    assert not any(f.endswith(".turn") for f in os.listdir(out))
+    r = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="zero", stats_every=0, log_every=0)
+    r.read_restart(out + "G.h5.4", out + "DDV.h5.4", out + "U.bin.4")
+    pr, orr, ur = r.get_state()
+    assert np.array_equal(pr, p4) and np.array_equal(orr, o4) and np.array_equal(ur, u4)
+    assert r.steps_done() == 4
+
+
+def test_symmetrize_with_communicator_matches_single_rank(native):
+    """Distributed kz=0 symmetrisation (column exchange) on a real 1-rank RCCL communicator equals the
+    single-rank kernel bitwise and leaves the kz=0 plane Hermitian."""
+    kw = dict(NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="zero", stats_every=0, log_every=0,
+              symmetry_every=0)
+    o = ora.OracleSolver(32, 33, 17, Re=400.0)
+    phi, om = ora.random_state(o.plan, o.ops, seed=7, amp=0.3)
+    rng = np.random.default_rng(3)
+    phi[:, :, 0] += 0.01 * (rng.standard_normal(phi[:, :, 0].shape) + 1j * rng.standard_normal(phi[:, :, 0].shape))
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    res = []
+    for uid in (b"", native.new_unique_id()):
+        s = native.Solver(default_config(**kw), 0, 1, 0, uid)
+        s.set_state(phi, om, U)
+        s.symmetrize()
+        res.append(s.get_state())
+    (pa, oa, _), (pb, ob, _) = res
+    assert np.array_equal(pa, pb) and np.array_equal(oa, ob)
+    nkx = pa.shape[1]
+    for k in range(1, nkx):
+        assert np.array_equal(pa[:, k, 0], np.conj(pa[:, nkx - k, 0]))
+    assert not np.any(pa[:, 0, 0].imag)

@@ -29,19 +29,7 @@ import numpy as np  # noqa: E402
 
 from channel_gpu_amd.models.channel import ChannelFlow  # noqa: E402
 from channel_gpu_amd.utils.config import load_config  # noqa: E402
-
-
-def save_snapshot(flow: ChannelFlow, path: str, step: int, t: float):
-    phi, om, U = flow.get_state()
-    np.savez_compressed(path, phi=phi.astype(np.complex64), om=om.astype(np.complex64), U=U, step=step, time=t,
-                        NX=flow.cfg.NX, NY=flow.cfg.NY, NZ=flow.cfg.NZ, Re=flow.cfg.Re)
-
-
-def load_snapshot(flow: ChannelFlow, path: str):
-    d = np.load(path)  # allow_pickle=False (default): plain arrays only
-    flow.set_state(d["phi"].astype(np.complex128), d["om"].astype(np.complex128), d["U"])
-    flow.solver.set_time(float(d["time"]), 0.0)
-    return int(d["step"]), float(d["time"])
+from channel_gpu_amd.utils.snapshots import export_seed, load_snapshot, save_snapshot  # noqa: E402
 
 
 def main() -> int:
@@ -53,9 +41,14 @@ def main() -> int:
     ap.add_argument("--average", type=int, default=120000, help="averaging steps")
     ap.add_argument("--sample-every", type=int, default=10)
     ap.add_argument("--log-every", type=int, default=1000)
-    ap.add_argument("--amplitude", type=float, default=0.5, help="random IC amplitude")
+    ap.add_argument("--amplitude", type=float, default=0.05, help="random IC amplitude (per mode)")
     ap.add_argument("--resume", default="", help="state_fp32.npz to start from instead of the random IC")
+    ap.add_argument("--export-seed", nargs=2, metavar=("STATE_NPZ", "OUT_NPZ"),
+                    help="write the compact regression-test seed of a state file and exit")
     a = ap.parse_args()
+    if a.export_seed:
+        export_seed(*a.export_seed)
+        return 0
 
     os.makedirs(a.out, exist_ok=True)
     path = os.path.abspath(a.out) + "/"
@@ -65,7 +58,9 @@ def main() -> int:
     s = flow.solver
     step0, t0 = 0, 0.0
     if a.resume:
-        step0, t0 = load_snapshot(flow, a.resume)
+        phi, om, U, step0, t0 = load_snapshot(a.resume)
+        flow.set_state(phi, om, U)
+        s.set_time(t0, 0.0)
     else:
         flow.initialize()
     y = np.asarray(s.grid.y)
@@ -119,7 +114,7 @@ def main() -> int:
     with open(path + "summary.json", "w") as f:
         json.dump(summary, f, indent=1)
     L = s.log()
-    save_snapshot(flow, path + "state_fp32.npz", step0 + n + m, L.time)
+    save_snapshot(path + "state_fp32.npz", *flow.get_state(), step=step0 + n + m, time=L.time, cfg=cfg)
     print(json.dumps(summary), flush=True)
     return 0
 
