@@ -554,7 +554,8 @@ void Solver::transforms(int n, bool /*stats*/) {
   za.inv_dy = d_invdy_;
   za.cx = p.ax * p.Kx;
   za.cz = p.az * p.Kz;
-  za.maxima = d_max_;
+  // CFL maxima of the current state only (substep 0, as calcDt at RK3.c:143-145); substeps 1, 2 skip them
+  za.maxima = n == 0 ? d_max_ : nullptr;
   DtArgs da;
   da.maxima = d_max_;
   da.dt = d_dt_;
