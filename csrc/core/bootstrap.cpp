@@ -4,12 +4,14 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -73,14 +75,44 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
     sockaddr_in sa{};
     sa.sin_family = AF_INET;
     sa.sin_port = htons(static_cast<uint16_t>(port));
+    // listen on MASTER_ADDR (the address the peers connect to), not on every interface
     sa.sin_addr.s_addr = htonl(INADDR_ANY);
-    CH_CHECK(::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0, "bind to port " << port << " failed");
+    {
+      addrinfo hints{}, *res = nullptr;
+      hints.ai_family = AF_INET;
+      hints.ai_socktype = SOCK_STREAM;
+      if (getaddrinfo(addr.c_str(), nullptr, &hints, &res) == 0 && res) {
+        sa.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+        freeaddrinfo(res);
+      }
+    }
+    CH_CHECK(::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0,
+             "bind to " << addr << ":" << port << " failed");
     CH_CHECK(::listen(ls, pi.size) == 0, "listen failed");
+    std::vector<bool> seen(pi.size, false);
+    seen[0] = true;
     for (int i = 1; i < pi.size; ++i) {
+      // bounded wait: a peer that died before connecting is an error, not a hang
+      pollfd pf{ls, POLLIN, 0};
+      int left_ms = 0;
+      while (true) {
+        left_ms = static_cast<int>(std::chrono::duration_cast<std::chrono::milliseconds>(
+                                       deadline - std::chrono::steady_clock::now()).count());
+        CH_CHECK(left_ms > 0, "bootstrap: only " << i - 1 << " of " << pi.size - 1 << " peers connected within "
+                                                 << timeout_s << " s");
+        const int pr = ::poll(&pf, 1, std::min(left_ms, 1000));
+        if (pr > 0) break;
+      }
       int fd = ::accept(ls, nullptr, nullptr);
       CH_CHECK(fd >= 0, "accept failed");
+      timeval tv{};
+      tv.tv_sec = std::max(1, left_ms / 1000);
+      setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
       int32_t peer = -1;
       recv_all(fd, &peer, sizeof(peer));
+      CH_CHECK(peer > 0 && peer < pi.size && !seen[peer],
+               "bootstrap: unexpected peer rank " << peer << " (world size " << pi.size << ")");
+      seen[peer] = true;
       const uint64_t n = payload.size();
       send_all(fd, &n, sizeof(n));
       send_all(fd, payload.data(), payload.size());

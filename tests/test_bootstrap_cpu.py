@@ -39,3 +39,50 @@ def test_shm_uid_shared_over_gloo():
         mp.start_processes(_worker, args=(2, _free_port(), d), nprocs=2, join=True, start_method="spawn")
         ids = [open(os.path.join(d, f"uid{r}"), "rb").read() for r in range(2)]
     assert ids[0] == ids[1] and ids[0].startswith(b"shm:channel_")
+
+
+_TCP_SCRIPT = r"""
+import os, sys
+sys.path.insert(0, os.environ["CHANNEL_ROOT"])
+from channel_gpu_amd import require_core
+C = require_core()
+pi = C.ProcInfo.from_env()
+out = C.tcp_broadcast(pi, b"payload-from-0" if pi.rank == 0 else b"", int(os.environ.get("TMO", "30")))
+print("GOT", out.decode(), flush=True)
+"""
+
+
+def _tcp_env(rank, world, port):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(port), CHANNEL_ROOT=root, CHANNEL_TORCH_FREE="1")
+
+
+def test_native_tcp_broadcast_three_ranks():
+    """The torch-free rendezvous of bench.py / the drivers: rank 0's payload reaches every rank."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, "-c", _TCP_SCRIPT], env=_tcp_env(r, 3, port), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(3)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    assert all("GOT payload-from-0" in o for o, _ in outs)
+
+
+def test_native_tcp_broadcast_missing_peer_times_out():
+    """Rank 0 waits a bounded time for its peers (a dead peer is an error, not a hang)."""
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(_tcp_env(0, 3, port), TMO="2")
+    r = subprocess.run([sys.executable, "-c", _TCP_SCRIPT], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "peers connected" in r.stderr
