@@ -71,13 +71,13 @@ void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t
 // Per-pass FFT twiddle tables for length n (FftPlan T1/T2 layout, fft_device.hpp), fp32 or fp64.
 struct Twiddles {
   void* buf = nullptr;
+  void* reg = nullptr;  // n = 1024: [M][64] W_N^(n1 k2), [4][16] W_64^(a c) of the register z stage
   int n = 0;
   bool fp64 = false;
   void build(int n, bool fp64);
   void release();
   ~Twiddles() { release(); }
 };
-
 // Source of a spectral field for the backward x-transform: for P ranks the blocks received from
 // each source rank s hold [y_local][nkx_s][nkz] starting at element offset off[s].
 // Block self_seg (this rank's own kx range, if >= 0) lives at self_base + f * self_field_stride

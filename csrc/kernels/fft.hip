@@ -27,6 +27,8 @@ namespace channel {
 
 using namespace dev;
 
+static void build_reg_twiddles(int n, bool fp64, void** out);
+
 void Twiddles::build(int n_, bool fp64_) {
   release();
   n = n_;
@@ -44,11 +46,13 @@ void Twiddles::build(int n_, bool fp64_) {
     HIP_CHECK(hipMalloc(&buf, sz * sizeof(float2)));
     HIP_CHECK(hipMemcpy(buf, hf.data(), sz * sizeof(float2), hipMemcpyHostToDevice));
   }
+  if (n == 1024) build_reg_twiddles(n, fp64, &reg);
 }
 
 void Twiddles::release() {
   if (buf) (void)hipFree(buf);
-  buf = nullptr;
+  if (reg) (void)hipFree(reg);
+  buf = reg = nullptr;
 }
 
 // ---- x-direction -------------------------------------------------------------------------
@@ -530,6 +534,274 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   }
 }
 
+// ---- register-resident z stage (NZP = 64 M, M = 16: the 1024-point rows of the headline grid) --
+// The LDS-pass FFT above makes 4 LDS round trips per transform (gather, 3 Stockham passes) and is
+// latency-bound at 2 waves/SIMD.  Here each transform is a four-step FFT N = M x 64 held in the
+// wave's registers: lane k2 owns Z[k2 + 64 k1] (loaded straight from global memory, conjugate
+// mirror included), an M-point DFT in registers, a twiddle, ONE LDS transpose, a 16-point DFT in
+// registers, a twiddle and a 4-point DFT across the lanes of a quad (DPP quad_perm, no LDS).  The
+// physical row stays in registers in the permuted order n = n1 + M (c + 16 br(a)), which is exactly
+// the input order of the reverse network used for the forward transforms of H.
+constexpr int kQuadXor1 = 0xB1;  // DPP quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;  // DPP quad_perm [2,3,0,1]
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+template <int CTRL, typename T2>
+__device__ __forceinline__ T2 quad_swap(T2 v) {
+  return T2{dpp_mov<CTRL>(v.x), dpp_mov<CTRL>(v.y)};
+}
+// one radix-2 stage across a lane pair: low lane a + b, high lane a - b (b = partner's value)
+template <int CTRL, typename T2>
+__device__ __forceinline__ T2 quad_bfly(T2 v, bool high) {
+  using T = decltype(v.x);
+  const T2 p = quad_swap<CTRL>(v);
+  const T s = high ? T(-1) : T(1);
+  return T2{p.x + s * v.x, p.y + s * v.y};
+}
+// natural order in (lane a of the quad holds y_a) -> lane a holds Y[br(a)] (br swaps 1 and 2)
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 quad_dft4_nat_in(T2 v, int a) {
+  v = quad_bfly<kQuadXor2>(v, (a & 2) != 0);
+  if (a == 3) v = mul_mi<INV>(v);
+  return quad_bfly<kQuadXor1>(v, (a & 1) != 0);
+}
+// bit-reversed order in (lane a holds y_br(a)) -> natural order out (lane a holds Y[a])
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 quad_dft4_br_in(T2 v, int a) {
+  v = quad_bfly<kQuadXor1>(v, (a & 1) != 0);
+  if (a == 3) v = mul_mi<INV>(v);
+  return quad_bfly<kQuadXor2>(v, (a & 2) != 0);
+}
+template <typename T2>
+__device__ __forceinline__ T2 cmulc(T2 a, T2 w) {  // a * conj(w)
+  return T2{a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y};
+}
+
+constexpr int kRegPitch = 68;  // transpose row pitch (64 + 4): conflict-free b64 column reads
+
+// Inverse transform of one spectral row held as z[k1] = Z[lane + 64 k1] (unnormalised, +i sign);
+// on return z[c] = x[n1 + M (c + 16 br(a))], lane = 4 g + a, n1 = g (M = 16).
+// buf: this wave's M x kRegPitch transpose buffer; tw1: [M][64] W_N^(n1 k2); tw64: [4][16] W_64^(a c).
+template <int M, typename T2>
+__device__ __forceinline__ void reg_fft_inv(T2 (&z)[M], T2* buf, const T2* tw1, const T2* tw64, int lane) {
+  static_assert(M == 16, "register z-stage FFT: M = 16 (N = 1024)");
+  dft16<true>(z);  // over k1 -> n1
+#pragma unroll
+  for (int n1 = 1; n1 < M; ++n1) z[n1] = cmulc(z[n1], tw1[n1 * 64 + lane]);
+#pragma unroll
+  for (int n1 = 0; n1 < M; ++n1) buf[n1 * kRegPitch + lane] = z[n1];
+  __builtin_amdgcn_wave_barrier();
+  const int g = lane >> 2, a = lane & 3;
+#pragma unroll
+  for (int b = 0; b < 16; ++b) z[b] = buf[g * kRegPitch + a + 4 * b];
+  __builtin_amdgcn_wave_barrier();
+  dft16<true>(z);  // over b -> c
+#pragma unroll
+  for (int c = 1; c < 16; ++c)
+    if (a != 0) z[c] = cmulc(z[c], tw64[a * 16 + c]);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) z[c] = quad_dft4_nat_in<true>(z[c], a);
+}
+
+// Forward transform of a physical row in the register order produced by reg_fft_inv; on return
+// z[k1] = Z[lane + 64 k1] (unnormalised, -i sign).
+template <int M, typename T2>
+__device__ __forceinline__ void reg_fft_fwd(T2 (&z)[M], T2* buf, const T2* tw1, const T2* tw64, int lane) {
+  static_assert(M == 16, "register z-stage FFT: M = 16 (N = 1024)");
+  const int g = lane >> 2, a = lane & 3;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) z[c] = quad_dft4_br_in<false>(z[c], a);  // over d -> e = a
+#pragma unroll
+  for (int c = 1; c < 16; ++c)
+    if (a != 0) z[c] = cmul(z[c], tw64[a * 16 + c]);
+  dft16<false>(z);  // over c -> f
+#pragma unroll
+  for (int f = 0; f < 16; ++f) buf[g * kRegPitch + a + 4 * f] = z[f];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int n1 = 0; n1 < M; ++n1) z[n1] = buf[n1 * kRegPitch + lane];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int n1 = 1; n1 < M; ++n1) z[n1] = cmul(z[n1], tw1[n1 * 64 + lane]);
+  dft16<false>(z);  // over n1 -> k1
+}
+
+template <int M, typename T, bool SEG>
+__global__ void __launch_bounds__(256) zphys_reg_kernel(ZArgs a, typename C2<T>::type* fields,
+                                                        const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  constexpr int NZP = 64 * M;
+  __shared__ T2 tbuf[ZW][M * kRegPitch];
+  __shared__ T2 tws[NZP + 64];  // [M][64] W_N^(n1 k2), then [4][16] W_64^(a c)
+  __shared__ float red[4][ZW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < NZP + 64; i += ZW * 64) tws[i] = tw[i];
+  __syncthreads();
+  const T2* tw1 = tws;
+  const T2* tw64 = tws + NZP;
+  T2* buf = tbuf[w];
+  const long long nrows = static_cast<long long>(a.ny) * a.NX;
+  const long long r = static_cast<long long>(blockIdx.x) * ZW + w;
+  const int nkz = a.nkz;
+  const long long fs = a.field_stride;
+  float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
+  auto zaddr = [&](int k) -> long long {
+    if constexpr (SEG) {
+      const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
+      return sp.off + r * sp.count + (k - sp.start);
+    } else {
+      return r * nkz + k;
+    }
+  };
+
+  if (r < nrows) {  // wave-uniform
+    T2 ph[3][M];
+    // Only the retained half is loaded (slot i = mode lane + 64 i, i < M/2); the conjugate mirror
+    // Z_{N-k} comes from lane 64 - lane (slot M-1-k1; lane 0: its own slot M-k1) by a lane
+    // permute.  The loads of field pair p+1 are issued before the transform of pair p.
+    constexpr int MH = M / 2;
+    T2 la[2][MH], lb[2][MH];
+    auto load_pair = [&](int p, T2 (&va)[MH], T2 (&vb)[MH]) {
+      const T2* A = fields + (2 * p) * fs;
+      const T2* B = fields + (2 * p + 1) * fs;
+#pragma unroll
+      for (int i = 0; i < MH; ++i) {
+        const int k = lane + 64 * i;
+        const bool ok = k < nkz;
+        const long long o = ok ? zaddr(k) : 0;
+        va[i] = ok ? A[o] : T2{0, 0};
+        vb[i] = ok ? B[o] : T2{0, 0};
+      }
+    };
+    load_pair(0, la[0], lb[0]);
+    const int src = (64 - lane) & 63;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int cur = p & 1;
+      if (p < 2) load_pair(p + 1, la[cur ^ 1], lb[cur ^ 1]);
+      // Z_k = A_k + i B_k (k < nkz), Z_{N-k} = conj(A_k) + i conj(B_k); kz = 0 imaginary parts dropped
+#pragma unroll
+      for (int k1 = 0; k1 < MH; ++k1) {
+        const T2 A = la[cur][k1], B = lb[cur][k1];
+        ph[p][k1] = (lane == 0 && k1 == 0) ? T2{A.x, B.x} : T2{A.x - B.y, A.y + B.x};
+      }
+#pragma unroll
+      for (int k1 = MH; k1 < M; ++k1) {
+        T2 A{__shfl(la[cur][M - 1 - k1].x, src), __shfl(la[cur][M - 1 - k1].y, src)};
+        T2 B{__shfl(lb[cur][M - 1 - k1].x, src), __shfl(lb[cur][M - 1 - k1].y, src)};
+        if (lane == 0) {  // N - k = 64 (M - k1): own slot M - k1 (k1 = M/2 is the Nyquist mode: zero)
+          A = k1 > MH ? la[cur][(M - k1) % MH] : T2{0, 0};
+          B = k1 > MH ? lb[cur][(M - k1) % MH] : T2{0, 0};
+        }
+        ph[p][k1] = T2{A.x + B.y, B.x - A.y};
+      }
+      if (!(a.diag & 1)) reg_fft_inv<M>(ph[p], buf, tw1, tw64, lane);
+    }
+    // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
+    const int yl = static_cast<int>(r / a.NX);
+    const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    T2 hxy[M], hz[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const T u = ph[0][i].x, v = ph[0][i].y, ww = ph[1][i].x, wx = ph[1][i].y, wy = ph[2][i].x, wz = ph[2][i].y;
+      hxy[i] = T2{v * wz - ww * wy, ww * wx - u * wz};
+      hz[i] = T2{u * wy - v * wx, T(0)};
+      const float au = fabsf(static_cast<float>(u)), av = fabsf(static_cast<float>(v)), aw = fabsf(static_cast<float>(ww));
+      mu = fmaxf(mu, au);
+      mv = fmaxf(mv, av);
+      mw = fmaxf(mw, aw);
+      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+    }
+    if (!(a.diag & 1)) {
+      reg_fft_fwd<M>(hxy, buf, tw1, tw64, lane);
+      reg_fft_fwd<M>(hz, buf, tw1, tw64, lane);
+    }
+    // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i); Z_{N-k}
+    // lives in lane 64 - lane at k1' = M-1-k1 (lane 0: its own k1' = M - k1)
+    const T sc = static_cast<T>(0.5 * a.scale), sz = static_cast<T>(a.scale);
+    constexpr int MKO = (NZP / 2 + 63) / 64;
+#pragma unroll
+    for (int k1 = 0; k1 < MKO; ++k1) {
+      const int k = lane + 64 * k1;
+      const int src = (64 - lane) & 63;
+      T2 zm{__shfl(hxy[M - 1 - k1].x, src), __shfl(hxy[M - 1 - k1].y, src)};
+      if (lane == 0) zm = hxy[(M - k1) % M];
+      if (k < nkz) {
+        const T2 Z = hxy[k1];
+        const long long o = zaddr(k);
+        fields[0 * fs + o] = T2{(Z.x + zm.x) * sc, (Z.y - zm.y) * sc};
+        fields[1 * fs + o] = T2{(Z.y + zm.y) * sc, -(Z.x - zm.x) * sc};
+        fields[2 * fs + o] = T2{hz[k1].x * sz, hz[k1].y * sz};
+      }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    mu = fmaxf(mu, __shfl_xor(mu, o));
+    mv = fmaxf(mv, __shfl_xor(mv, o));
+    mw = fmaxf(mw, __shfl_xor(mw, o));
+    mc = fmaxf(mc, __shfl_xor(mc, o));
+  }
+  if (lane == 0) {
+    red[0][w] = mu;
+    red[1][w] = mv;
+    red[2][w] = mw;
+    red[3][w] = mc;
+  }
+  __syncthreads();
+  if (tid < 4 && a.maxima) {
+    float m = 0.f;
+    for (int i = 0; i < ZW; ++i) m = fmaxf(m, red[tid][i]);
+    atomic_max_pos(&a.maxima[tid], m);
+  }
+}
+
+// twiddles of the register z stage: [M][64] W_N^(n1 k2) then [4][16] W_64^(a c) (forward sign)
+static void build_reg_twiddles(int n, bool fp64, void** out) {
+  const int M = n / 64;
+  const double two_pi = 2.0 * std::acos(-1.0);
+  std::vector<double2> h(n + 64);
+  for (int n1 = 0; n1 < M; ++n1)
+    for (int k2 = 0; k2 < 64; ++k2) {
+      const double ang = -two_pi * static_cast<double>(n1 * k2) / n;
+      h[n1 * 64 + k2] = double2{std::cos(ang), std::sin(ang)};
+    }
+  for (int aa = 0; aa < 4; ++aa)
+    for (int c = 0; c < 16; ++c) {
+      const double ang = -two_pi * static_cast<double>(aa * c) / 64.0;
+      h[n + aa * 16 + c] = double2{std::cos(ang), std::sin(ang)};
+    }
+  if (fp64) {
+    HIP_CHECK(hipMalloc(out, h.size() * sizeof(double2)));
+    HIP_CHECK(hipMemcpy(*out, h.data(), h.size() * sizeof(double2), hipMemcpyHostToDevice));
+  } else {
+    std::vector<float2> hf(h.size());
+    for (size_t i = 0; i < h.size(); ++i) hf[i] = float2{static_cast<float>(h[i].x), static_cast<float>(h[i].y)};
+    HIP_CHECK(hipMalloc(out, hf.size() * sizeof(float2)));
+    HIP_CHECK(hipMemcpy(*out, hf.data(), hf.size() * sizeof(float2), hipMemcpyHostToDevice));
+  }
+}
+
+// CHANNEL_ZREG=1 selects the register-resident z stage at Nzp = 1024.  Measured at 1024x385x1024
+// fp32 (r2p): 3.5x fewer LDS instructions than the LDS-pass kernel but +17 % VALU and +65 %
+// wave-parked cycles (one transpose wait + per-FFT twiddle reads per transform at 2 waves/SIMD):
+// 51.2 vs 50.0 ms/step, so the LDS-pass kernel stays the default.
+static bool zreg_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_ZREG");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <typename T>
 static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
@@ -563,6 +835,28 @@ void zphys(const ZArgs& a_in, void* fields, const Twiddles& tw, bool fp64, hipSt
   CH_CHECK(tw.n == a.Nzp && tw.fp64 == fp64, "zphys: twiddle table mismatch");
   CH_CHECK(a.nkz - 1 < a.Nzp / 2, "zphys: retained kz must be below Nyquist");
   if (a.ny == 0) return;
+  if (a.Nzp == 1024 && zreg_enabled()) {
+    CH_CHECK(tw.reg, "zphys: register-FFT twiddles missing");
+    const long long nrows = static_cast<long long>(a.ny) * a.NX;
+    dim3 grid(static_cast<unsigned>((nrows + ZW - 1) / ZW));
+    if (fp64) {
+      if (a.nseg > 1)
+        hipLaunchKernelGGL((zphys_reg_kernel<16, double, true>), grid, dim3(256), 0, s, a, static_cast<double2*>(fields),
+                           static_cast<const double2*>(tw.reg));
+      else
+        hipLaunchKernelGGL((zphys_reg_kernel<16, double, false>), grid, dim3(256), 0, s, a,
+                           static_cast<double2*>(fields), static_cast<const double2*>(tw.reg));
+    } else {
+      if (a.nseg > 1)
+        hipLaunchKernelGGL((zphys_reg_kernel<16, float, true>), grid, dim3(256), 0, s, a, static_cast<float2*>(fields),
+                           static_cast<const float2*>(tw.reg));
+      else
+        hipLaunchKernelGGL((zphys_reg_kernel<16, float, false>), grid, dim3(256), 0, s, a, static_cast<float2*>(fields),
+                           static_cast<const float2*>(tw.reg));
+    }
+    HIP_LAUNCH_CHECK(s);
+    return;
+  }
   if (fp64) zphys_launch<double>(a, fields, tw, s);
   else zphys_launch<float>(a, fields, tw, s);
 }

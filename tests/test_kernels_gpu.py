@@ -79,9 +79,10 @@ def test_xfft(native, NX, nkz, dtype):
 
 
 @pytest.mark.parametrize("NX,Nzp,dtype", [(32, 32, torch.complex128), (64, 128, torch.complex64),
-                                          (16, 1024, torch.complex64), (32, 2048, torch.complex64),
-                                          (16, 512, torch.complex128)])
+                                          (16, 1024, torch.complex64), (16, 1024, torch.complex128),
+                                          (32, 2048, torch.complex64), (16, 512, torch.complex128)])
 def test_zphys(native, NX, Nzp, dtype):
+    """z stage vs NumPy (LDS-pass kernel; the register-resident one is covered in a subprocess)."""
     rng = np.random.default_rng(Nzp)
     nkz = Nzp // 3 + 1
     ny = 3
@@ -101,3 +102,40 @@ def test_zphys(native, NX, Nzp, dtype):
     assert abs(m[0] - np.abs(u).max()) < 1e-4 * np.abs(u).max()
     assert abs(m[1] - np.abs(v).max()) < 1e-4 * np.abs(v).max()
     assert abs(m[3] - (np.abs(u) + np.abs(v) + np.abs(w)).max()) < 1e-4 * m[3]
+
+
+ZREG_SCRIPT = r"""
+import os, sys
+import numpy as np, torch
+sys.path.insert(0, os.environ["CHANNEL_ROOT"])
+from channel_gpu_amd import require_native
+C = require_native()
+rng = np.random.default_rng(3)
+for dtype, tol in ((torch.complex64, 5e-6), (torch.complex128, 1e-12)):
+    NX, Nzp, ny = 16, 1024, 3
+    nkz = Nzp // 3 + 1
+    f = rng.standard_normal((6, ny, NX, nkz)) + 1j * rng.standard_normal((6, ny, NX, nkz))
+    f[..., 0] = f[..., 0].real
+    H, m = C.zphys(torch.tensor(f, dtype=dtype, device="cuda"), Nzp, torch.ones(ny, dtype=torch.float64), 1.0, 1.0)
+    phys = np.fft.irfft(np.concatenate([f, np.zeros(f.shape[:-1] + (Nzp // 2 + 1 - nkz,))], -1), n=Nzp, axis=-1,
+                        norm="forward")
+    u, v, w, wx, wy, wz = phys
+    Hp = np.stack([v * wz - w * wy, w * wx - u * wz, u * wy - v * wx])
+    Href = np.fft.rfft(Hp, axis=-1, norm="forward")[..., :nkz] / NX
+    e = np.linalg.norm(H.cpu().numpy() - Href) / np.linalg.norm(Href)
+    assert e < tol, (dtype, e)
+    assert abs(m.cpu().numpy()[0] - np.abs(u).max()) < 1e-4 * np.abs(u).max()
+print("ZREG_OK")
+"""
+
+
+def test_zphys_register_kernel():
+    """CHANNEL_ZREG=1: register-resident four-step z stage (Nzp = 1024, fp32/fp64) vs NumPy."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CHANNEL_ZREG="1", CHANNEL_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", ZREG_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ZREG_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
