@@ -292,12 +292,16 @@ class OracleSolver:
     """
 
     def __init__(self, NX, NY, NZ, Re=3250.0, Q=1.8, LX=2 * math.pi, LZ=math.pi, stretch=2.0, cfl=0.5,
-                 dt_max=0.05, dt_fixed=0.0, P=1, rank=0, dist=None, Pr=1):
+                 dt_max=0.05, dt_fixed=0.0, P=1, rank=0, dist=None, Pr=1, explicit_d2="compact",
+                 influence="discrete"):
         self.plan = OraclePlan(NX, NY, NZ, P, rank, LX, LZ, Pr)
         self.ops = build_ops(NY, stretch)
         self.Re, self.nu, self.Q = Re, 1.0 / Re, Q
         self.cfl, self.dt_max, self.dt_fixed = cfl, dt_max, dt_fixed
         self.dist = dist
+        # reference-parity switches: explicit D2 as D1 o D1 (RK3_kernels.cu:160-164) and analytic
+        # cosh/sinh influence functions (bilplacSolver_double.cu:56-250, l1/l2 typo fixed)
+        self.explicit_d2, self.influence = explicit_d2, influence
         p = self.plan
         shape = (NY, p.nkx_loc, p.nkz_loc)
         self.phi = np.zeros(shape, complex)
@@ -458,7 +462,14 @@ class OracleSolver:
         Rp_prev, Rw_prev = self.lines(self.Rphi), self.lines(self.Rom)
 
         def rhs(q, Rn, Rp):
-            return ops.M @ q + dt * (ALPHA[n] * nu * (ops.K @ q - k2 * (ops.M @ q)) + GAMMA[n] * Rn + ZETA[n] * Rp)
+            Kq = ops.K @ q
+            if self.explicit_d2 == "dd":
+                Kdd = ops.M @ (ops.D1 @ (ops.D1 @ q))
+                Kdd[0] = Kdd[-1] = 0.0  # interior rows only, like K
+                if m is not None:
+                    Kdd[:, m] = Kq[:, m]  # the mean profile keeps the compact D2
+                Kq = Kdd
+            return ops.M @ q + dt * (ALPHA[n] * nu * (Kq - k2 * (ops.M @ q)) + GAMMA[n] * Rn + ZETA[n] * Rp)
 
         rP = rhs(phi_l, RPn, Rp_prev)
         rW = rhs(om_l, RWn, Rw_prev)
@@ -483,6 +494,8 @@ class OracleSolver:
         vp = _bsolve(Ah, ops.M @ phi_p)
         vh1, vh2 = _bsolve(Ah, ops.M @ ph1), _bsolve(Ah, ops.M @ ph2)
         dvp, dvh1, dvh2 = ops.D1 @ vp, ops.D1 @ vh1, ops.D1 @ vh2
+        if self.influence == "analytic" and dt > 1e-14:
+            ph1, ph2, vh1, vh2, dvh1, dvh2 = analytic_influence(ops.y, k2, BETA[n] * dt * nu)
         det = dvh1[0] * dvh2[-1] - dvh2[0] * dvh1[-1]
         ok = (k2 > 0) & (dt > 1e-14) & (det != 0)
         dets = np.where(ok, det, 1.0)
@@ -533,6 +546,36 @@ class OracleSolver:
             wgt[self.mean_line] = 0
         return np.stack([(np.abs(u) ** 2) @ wgt, (np.abs(v) ** 2) @ wgt, (np.abs(w) ** 2) @ wgt,
                          (u.real * v.real + u.imag * v.imag) @ wgt])
+
+
+def _chs(l, y):
+    """cosh(l y)/cosh(l), sinh(l y)/sinh(l) and their y-derivatives, overflow-safe (l > 0)."""
+    ep, em, e2 = np.exp(l * (y - 1.0)), np.exp(-l * (y + 1.0)), np.exp(-2.0 * l)
+    return (ep + em) / (1 + e2), (ep - em) / (1 - e2), l * (ep - em) / (1 + e2), l * (ep + em) / (1 - e2)
+
+
+def analytic_influence(y: np.ndarray, k2: np.ndarray, c: float):
+    """Analytic homogeneous solutions of the phi-v system for each line (reference
+    bilplacSolver_double.cu:56-217 with the l1/l2 typo fixed): phi1,2 = (C_l1 -+ S_l1)/2 with
+    l1^2 = k^2 + 1/c (c = beta dt nu), v1,2 = D [(C_l1 -+ S_l1)/2 - (C_l2 -+ S_l2)/2] with l2 = k,
+    D = 1/(l1^2 - l2^2); returns (phi1, phi2, v1, v2, dv1, dv2) as [NY, lines] (dv: analytic, only the
+    wall rows are used).  Lines with k = 0 get zeros."""
+    yy = y[:, None]
+    ok = k2 > 0
+    l2 = np.sqrt(np.where(ok, k2, 1.0))[None, :]
+    l1 = np.sqrt(np.where(ok, k2, 1.0) + 1.0 / c)[None, :]
+    D = 1.0 / (l1 * l1 - l2 * l2)
+    C1, S1, dC1, dS1 = _chs(l1, yy)
+    C2, S2, dC2, dS2 = _chs(l2, yy)
+    ph1, ph2 = 0.5 * (C1 - S1), 0.5 * (C1 + S1)
+    v1 = D * (0.5 * (C1 - S1) - 0.5 * (C2 - S2))
+    v2 = D * (0.5 * (C1 + S1) - 0.5 * (C2 + S2))
+    dv1 = D * (0.5 * (dC1 - dS1) - 0.5 * (dC2 - dS2))
+    dv2 = D * (0.5 * (dC1 + dS1) - 0.5 * (dC2 + dS2))
+    z = ~ok
+    for a in (ph1, ph2, v1, v2, dv1, dv2):
+        a[:, z] = 0.0
+    return ph1, ph2, v1, v2, dv1, dv2
 
 
 def random_state(plan: OraclePlan, ops: YOps, seed: int = 1, amp: float = 0.1, kscale: float = 32.0):

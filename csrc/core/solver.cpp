@@ -213,6 +213,8 @@ void Solver::alloc() {
     invdy[j] = 1.0 / h;
   }
   HIP_CHECK(hipMemcpy(d_invdy_, invdy.data(), N * sizeof(double), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMalloc(&d_y_, N * sizeof(double)));
+  HIP_CHECK(hipMemcpy(d_y_, y.data(), N * sizeof(double), hipMemcpyHostToDevice));
   ev_a2a_.resize(6);
   ev_xf_.resize(6);
   ev_b_.resize(6);
@@ -245,9 +247,10 @@ void Solver::free_all() {
   step_ev_.clear();
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
     if (e) (void)hipEventDestroy(e);
-  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_})
+  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_, static_cast<void*>(d_y_)})
     if (p) (void)hipFree(p);
   state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = d_sym_ = nullptr;
+  d_y_ = nullptr;
 }
 
 void* Solver::field_ptr(int f) const {
@@ -408,6 +411,9 @@ void Solver::kspec(int mode, int n, bool stats) {
   a.dt = d_dt_;
   a.Q = cfg_.Q;
   a.forcing = cfg_.forcing == "parity" ? 1 : 0;
+  a.explicit_dd = cfg_.explicit_d2 == "dd";
+  a.analytic_influence = cfg_.influence == "analytic";
+  a.ygrid = d_y_;
   a.phi = field_ptr(PHI);
   a.omega = field_ptr(OMEGA);
   a.Rphi = field_ptr(RPHI);

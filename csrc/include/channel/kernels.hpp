@@ -52,6 +52,10 @@ struct SpecArgs {
   // mean flow forcing
   double Q = 1.8;
   int forcing = 0;        // 0 implicit (exact flux), 1 parity (constant add)
+  // reference-parity switches (config influence / explicit_d2; NY <= 256)
+  bool explicit_dd = false;          // explicit viscous D2 = D1 o D1
+  bool analytic_influence = false;   // cosh/sinh influence functions
+  const double* ygrid = nullptr;     // [N] y_j (analytic influence)
   // fields (T2* cast to void*)
   void* phi = nullptr;
   void* omega = nullptr;  // line (0,0) holds U(y)

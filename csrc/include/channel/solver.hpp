@@ -201,6 +201,7 @@ class Solver {
   int ychunk_ = 0;                 // y planes per x->z->x pipeline chunk (P = 1), 0 = whole slab
   double* d_invdy_ = nullptr;
   double* d_red_ = nullptr;  // one double for max_over_ranks
+  double* d_y_ = nullptr;    // y grid (analytic influence functions)
 
   std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;

@@ -381,7 +381,22 @@ __device__ __forceinline__ void czero(double (&x)[2][R]) {
     for (int r = 0; r < R; ++r) x[k][r] = 0.0;
 }
 
-template <int R, typename T, int W>
+// Reference-parity variants (compile-time, PAR bits): kParDD = explicit viscous D2 as D1 o D1
+// (RK3_kernels.cu:160-164, derivatives_nu_double.cu:440-446); kParAnalytic = analytic influence
+// functions (bilplacSolver_double.cu:56-250, l1/l2 typo fixed).  The default (PAR = 0) is the
+// compact D2 and discrete Green's functions.
+constexpr int kParDD = 1, kParAnalytic = 2;
+
+// overflow-safe cosh(l y)/cosh(l) and sinh(l y)/sinh(l) (and their y-derivatives), |y| <= 1, l > 0
+__device__ __forceinline__ void chs_profiles(double l, double y, double& C, double& S, double& dC, double& dS) {
+  const double ep = exp(l * (y - 1.0)), em = exp(-l * (y + 1.0)), e2 = exp(-2.0 * l);
+  C = (ep + em) / (1.0 + e2);
+  S = (ep - em) / (1.0 - e2);
+  dC = l * (ep - em) / (1.0 + e2);
+  dS = l * (ep + em) / (1.0 - e2);
+}
+
+template <int R, typename T, int W, int PAR = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
   // Coefficient tables (14 per-row tables + the D1 factorisation) are staged into LDS once per
@@ -543,9 +558,25 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     double rhsP[2][R], rhsW[2][R];
     {
       double q[2][R], Mq[2][R], Kq[2][R];
+      auto explicit_d2 = [&](double (&qq)[2][R]) {
+        if constexpr ((PAR & kParDD) != 0) {
+          if (!is_mean) {  // fluctuations: M (D1 o D1) q; the mean profile keeps the compact D2
+            double DD[2][R];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+              for (int r = 0; r < R; ++r) DD[k][r] = qq[k][r];
+            d1_apply<R, 2>(t, DD, lane);
+            d1_apply<R, 2>(t, DD, lane);
+            apply_M<R, 2>(t, DD, Kq, lane);
+            return;
+          }
+        }
+        apply_K<R, 2>(t, qq, Kq, lane);
+      };
       st.template commit<3>(q);  // phi
       apply_M<R, 2>(t, q, Mq, lane);
-      apply_K<R, 2>(t, q, Kq, lane);
+      explicit_d2(q);
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -553,7 +584,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           rhsP[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RPn[k][r]);
       st.template commit<4>(q);  // omega
       apply_M<R, 2>(t, q, Mq, lane);
-      apply_K<R, 2>(t, q, Kq, lane);
+      explicit_d2(q);
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -692,7 +723,42 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       wave_sum_n<8>(acc);
       const double p0r = acc[0], p0i = acc[1], pNr = acc[2], pNi = acc[3];
-      const double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
+      double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
+      if constexpr ((PAR & kParAnalytic) != 0) {
+        // analytic homogeneous solutions (bilplacSolver_double.cu:56-217): phi1,2 = (C_l1 -+ S_l1)/2,
+        // v1,2 = D [(C_l1 -+ S_l1)/2 - (C_l2 -+ S_l2)/2], l1^2 = k^2 + Re/(beta dt), l2 = k,
+        // D = 1/(l1^2 - l2^2); wall derivatives analytic, the particular one discrete
+        if (k2 > 0.0 && dt > 1e-14) {
+          const double l2 = sqrt(k2), l1 = sqrt(k2 + 1.0 / (a.rk_b * dt * a.nu)), Dd = 1.0 / (l1 * l1 - l2 * l2);
+          double dh[2][2];  // [solution][wall]
+#pragma unroll
+          for (int wall = 0; wall < 2; ++wall) {
+            const double yw = wall == 0 ? -1.0 : 1.0;
+            double C1_, S1_, dC1, dS1, C2_, S2_, dC2, dS2;
+            chs_profiles(l1, yw, C1_, S1_, dC1, dS1);
+            chs_profiles(l2, yw, C2_, S2_, dC2, dS2);
+            dh[0][wall] = Dd * (0.5 * (dC1 - dS1) - 0.5 * (dC2 - dS2));
+            dh[1][wall] = Dd * (0.5 * (dC1 + dS1) - 0.5 * (dC2 + dS2));
+          }
+          h10 = dh[0][0];
+          h1N = dh[0][1];
+          h20 = dh[1][0];
+          h2N = dh[1][1];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = lane * R + r;
+            const double yj = j < N ? a.ygrid[j] : 0.0;
+            double C1_, S1_, dC1, dS1, C2_, S2_, dC2, dS2;
+            chs_profiles(l1, yj, C1_, S1_, dC1, dS1);
+            chs_profiles(l2, yj, C2_, S2_, dC2, dS2);
+            const bool in = j < N;
+            phH[0][r] = in ? 0.5 * (C1_ - S1_) : 0.0;
+            phH[1][r] = in ? 0.5 * (C1_ + S1_) : 0.0;
+            vH[0][r] = in ? Dd * (0.5 * (C1_ - S1_) - 0.5 * (C2_ - S2_)) : 0.0;
+            vH[1][r] = in ? Dd * (0.5 * (C1_ + S1_) - 0.5 * (C2_ + S2_)) : 0.0;
+          }
+        }
+      }
       const double det = h10 * h2N - h20 * h1N;
       const bool apply = !is_mean && k2 > 0.0 && dt > 1e-14 && det != 0.0;
       const double id = apply ? 1.0 / det : 0.0;
@@ -869,18 +935,41 @@ constexpr int kspec_waves() {
   return (R <= 4 && 64 * R * 9 * 2 * sizeof(T) <= 64 * 1024) ? 8 : 4;
 }
 
-template <int R, typename T>
+template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_waves<R, T>();
-  auto kern = kspec_kernel<R, T, W>;
+  auto kern = kspec_kernel<R, T, W, PAR>;
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), W * 64))), block(W * 64);
   hipLaunchKernelGGL(kern, grid, block, 0, stream, t.tab, a);
 }
 
+template <int PAR>
+static void kspec_launch_par(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream) {
+  switch (t.R) {
+#define CH_PAR_R(RR)                                                  \
+  case RR:                                                            \
+    if (fp64) kspec_launch_t<RR, double, PAR>(t, a, stream);          \
+    else kspec_launch_t<RR, float, PAR>(t, a, stream);                \
+    break;
+    CH_PAR_R(1) CH_PAR_R(2) CH_PAR_R(3) CH_PAR_R(4)
+#undef CH_PAR_R
+    default: CH_CHECK(false, "reference-parity modes (influence=analytic, explicit_d2=dd) support NY <= 256");
+  }
+}
+
 void kspec_launch(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream) {
   CH_CHECK(a.N == t.tab.N, "kspec: NY mismatch with tables");
+  const int par = (a.explicit_dd ? kParDD : 0) | (a.analytic_influence ? kParAnalytic : 0);
+  if (par) {
+    CH_CHECK(!a.analytic_influence || a.ygrid, "kspec: analytic influence needs the y grid");
+    if (par == kParDD) kspec_launch_par<kParDD>(t, a, fp64, stream);
+    else if (par == kParAnalytic) kspec_launch_par<kParAnalytic>(t, a, fp64, stream);
+    else kspec_launch_par<kParDD | kParAnalytic>(t, a, fp64, stream);
+    HIP_LAUNCH_CHECK(stream);
+    return;
+  }
   if (fp64) {
     CH_DISPATCH_R(t.R, kspec_launch_t<R, double>(t, a, stream));
   } else {

@@ -71,3 +71,29 @@ def test_plane_stats_nonnegative():
     o.prepare()
     st = o.plane_stats()
     assert (st[:3] >= 0).all() and np.isfinite(st).all()
+
+
+def test_parity_modes_differ_from_default_but_stay_close():
+    """CPU oracle: explicit D1 o D1 and analytic influence functions (the reference's semantics) give
+    trajectories close to the default (compact D2, discrete Green's functions) but not identical; the
+    analytic influence only satisfies v'(+-1) = 0 to truncation error, the discrete one to round-off."""
+    NX, NY, NZ = 16, 33, 9
+    base = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=0.01)
+    phi, om = ora.random_state(base.plan, base.ops, seed=2, amp=0.3)
+    U = 0.75 * 1.8 * (1 - base.ops.y ** 2)
+    res = {}
+    for key in [("compact", "discrete"), ("dd", "discrete"), ("compact", "analytic")]:
+        o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=0.01, explicit_d2=key[0], influence=key[1])
+        o.set_state(phi, om, U)
+        for _ in range(2):
+            o.step()
+        res[key] = o
+    ref = res[("compact", "discrete")].phi
+    for key in [("dd", "discrete"), ("compact", "analytic")]:
+        d = np.linalg.norm(res[key].phi - ref) / np.linalg.norm(ref)
+        assert 1e-12 < d < 0.2, (key, d)
+    # wall derivative of v after the step: discrete influence -> round-off
+    o = res[("compact", "discrete")]
+    v = ora._bsolve(ora.helm_matrix(o.ops, o.k2), o.ops.M @ o.lines(o.phi))
+    dv = o.ops.D1 @ v
+    assert np.abs(dv[[0, -1]]).max() < 1e-9 * max(1.0, np.abs(v).max())

@@ -275,3 +275,27 @@ def test_symmetrize_with_communicator_matches_single_rank(native):
     for k in range(1, nkx):
         assert np.array_equal(pa[:, k, 0], np.conj(pa[:, nkx - k, 0]))
     assert not np.any(pa[:, 0, 0].imag)
+
+
+@pytest.mark.parametrize("explicit_d2,influence", [("dd", "discrete"), ("compact", "analytic"), ("dd", "analytic")])
+@pytest.mark.parametrize("NX,NY,NZ", [(32, 33, 17), (32, 65, 33)])
+def test_reference_parity_modes_match_oracle(native, explicit_d2, influence, NX, NY, NZ):
+    """Reference-parity switches: explicit_d2 = dd (D1 o D1, RK3_kernels.cu:160-164) and
+    influence = analytic (cosh/sinh Green's functions, bilplacSolver_double.cu:56-250) on the GPU vs
+    the NumPy oracle implementing the same semantics."""
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision="fp64", dt_fixed=0.01, stats_every=0, log_every=0,
+              symmetry_every=0, ic="zero", explicit_d2=explicit_d2, influence=influence)
+    s = make_solver(native, **kw)
+    o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=0.01, explicit_d2=explicit_d2, influence=influence)
+    phi, om = ora.random_state(o.plan, o.ops, seed=3, amp=0.3)
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    o.set_state(phi, om, U)
+    s.set_state(phi, om, U)
+    s.prepare()
+    for it in range(3):
+        o.step()
+        s.step(False)
+        gphi, gom, gU = s.get_state()
+        assert rel(gphi, o.phi) < 1e-9, f"phi step {it}: {rel(gphi, o.phi):.3e}"
+        assert rel(gom, o.om) < 1e-9, f"omega step {it}"
+        assert rel(gU, o.U) < 1e-11, f"U step {it}"
