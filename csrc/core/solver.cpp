@@ -205,7 +205,14 @@ void Solver::alloc() {
   // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
   // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
   if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
-  if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::atoi(ys);
+  if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::max(1, std::min(8, std::atoi(ys)));
+  for (int i = 2; i < ystreams_; ++i) {
+    hipStream_t st;
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    s_extra_.push_back(st);
+  }
+  ev_join_.resize(std::max(2, ystreams_));
+  for (auto& e : ev_join_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   std::vector<double> invdy(N);
   const auto& y = grid_.y;
   for (int j = 0; j < N; ++j) {
@@ -235,6 +242,10 @@ void Solver::free_all() {
   for (auto* v : {&ev_a2a_, &ev_xf_, &ev_b_, &ev_bb_})
     for (auto e : *v) (void)hipEventDestroy(e);
   for (auto e : tev_pool_) (void)hipEventDestroy(e);
+  for (auto e : ev_join_) (void)hipEventDestroy(e);
+  for (auto st : s_extra_) (void)hipStreamDestroy(st);
+  ev_join_.clear();
+  s_extra_.clear();
   for (auto* v : {&ev_cb_, &ev_cc_})
     for (auto e : *v) (void)hipEventDestroy(e);
   for (auto& pr : step_ev_) {
@@ -425,6 +436,8 @@ void Solver::kspec(int mode, int n, bool stats) {
   a.prof = kprof_on_ ? d_kprof_ : nullptr;
   if (stats) HIP_CHECK(hipMemsetAsync(d_stats_, 0, 4 * p.NY * sizeof(double), s_comp_));
   ev(0, false);
+  // (measured r2s: splitting this fused pass into an advance kernel and a prepare kernel frees no
+  // occupancy at R = 7 -- 481 and 348 registers -- and costs 10.2 vs 7.2 ms per substep)
   kspec_launch(ytab_, a, fp64_, s_comp_);
   ev(0, true);
   if (stats && comm_) {
@@ -600,16 +613,18 @@ void Solver::transforms(int n, bool /*stats*/) {
       // launch tail overlaps the next chunk's transforms (chunks are independent; the CFL maxima
       // are atomic)
       // (phase timing serialises the chunks on one stream so the stage times add up to the step)
-      const bool two = ystreams_ > 1 && !phase_timing_;
+      const int nst = phase_timing_ ? 1 : std::max(1, ystreams_);
+      std::vector<hipStream_t> streams = {s_comp_, s_comm_};
+      for (auto e : s_extra_) streams.push_back(e);
       roctxRangePushA("xzx_ychunked");
-      if (two) {
+      if (nst > 1) {
         HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
-        HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+        for (int i = 1; i < nst; ++i) HIP_CHECK(hipStreamWaitEvent(streams[i], ev_spec_, 0));
       }
       int ci = 0;
       for (int y0 = 0; y0 < p.ny_loc; y0 += ychunk_, ++ci) {
         const int ny = std::min(ychunk_, p.ny_loc - y0);
-        hipStream_t cs = (two && (ci & 1)) ? s_comm_ : s_comp_;
+        hipStream_t cs = streams[ci % nst];
         const size_t so = static_cast<size_t>(y0) * p.nkx * p.nkz * esz_;
         char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz * esz_;
         XArgs xc = xa;
@@ -633,9 +648,9 @@ void Solver::transforms(int n, bool /*stats*/) {
         xfft_forward(xc, ph, dc, tw_x_, fp64_, cs);
         ev(3, true, cs);
       }
-      if (two) {
-        HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
-        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+      for (int i = 1; i < nst; ++i) {
+        HIP_CHECK(hipEventRecord(ev_join_[i], streams[i]));
+        HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_join_[i], 0));
       }
       if (n == 0) dt_update(da, s_comp_);
       roctxRangePop();

@@ -197,7 +197,9 @@ class Solver {
   unsigned* d_health_ = nullptr;
   unsigned long long* d_kprof_ = nullptr;
   bool kprof_on_ = false;
-  int ystreams_ = 1;               // streams the y chunks alternate over
+  int ystreams_ = 1;               // streams the y chunks alternate over (P = 1)
+  std::vector<hipStream_t> s_extra_;   // streams beyond compute + comm for the chunk pipeline
+  std::vector<hipEvent_t> ev_join_;
   int ychunk_ = 0;                 // y planes per x->z->x pipeline chunk (P = 1), 0 = whole slab
   double* d_invdy_ = nullptr;
   double* d_red_ = nullptr;  // one double for max_over_ranks
