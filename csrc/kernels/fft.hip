@@ -56,16 +56,20 @@ void Twiddles::release() {
 }
 
 // ---- x-direction -------------------------------------------------------------------------
-constexpr int xcfg_c(int nx, int tsz) { return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 1024 ? 4 : 8); }
+// fp64 at NX = 2048: 2 columns per tile (the 4-column tile plus the twiddles would exceed the
+// 160 KB of LDS), one wave per column
+constexpr int xcfg_c(int nx, int tsz) {
+  return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 2048 ? 2 : (nx >= 1024 ? 4 : 8));
+}
 // WIDE = 1: twice the kz columns per tile (128-B row segments) with 512 threads and one block per
 // CU (the same 8 waves per CU); WIDE = 0: 64-B segments, 256 threads, two blocks per CU.
-constexpr int xcfg_nt(int wide) { return wide ? 512 : 256; }
+constexpr int xcfg_nt(int wide, int c = 4) { return wide ? 512 : (c >= 4 ? 256 : 64 * c); }
 constexpr int xcfg_minb(int wide) { return wide ? 1 : 2; }
 template <int NX, typename T, int WIDE = 0>
 struct XCfg {
   // kz columns per tile
   static constexpr int C = xcfg_c(NX, sizeof(T)) * (WIDE ? 2 : 1);
-  static constexpr int NT = xcfg_nt(WIDE);
+  static constexpr int NT = xcfg_nt(WIDE, C);
   // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
   // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
   static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
@@ -115,7 +119,7 @@ __device__ __forceinline__ SegPos seg_find(const int* start, const long long* of
 // the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
 template <int NX, typename T, bool SEG, int WIDE>
-__global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
@@ -198,7 +202,7 @@ __global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
 }
 
 template <int NX, typename T, bool SEG, int WIDE>
-__global__ void __launch_bounds__(xcfg_nt(WIDE), xcfg_minb(WIDE))
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
@@ -306,9 +310,7 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
 template <typename T>
 static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   CH_DISPATCH_N(a.NX, {
-    if constexpr (sizeof(T) == 8 && NN > 1024) {
-      CH_CHECK(false, "fp64 storage supports NX <= 1024");
-    } else if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
+    if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
       if (xwide_enabled()) xb_launch_cfg<NN, T, 1>(a, src, phys, tw, s);
       else xb_launch_cfg<NN, T, 0>(a, src, phys, tw, s);
     } else {
@@ -321,9 +323,7 @@ static void xb_launch(const XArgs& a, const XSrc& src, void* phys, const Twiddle
 template <typename T>
 static void xf_launch(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
   CH_DISPATCH_N(a.NX, {
-    if constexpr (sizeof(T) == 8 && NN > 1024) {
-      CH_CHECK(false, "fp64 storage supports NX <= 1024");
-    } else if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
+    if constexpr (sizeof(T) == 4 && NN >= 512 && NN <= 1024) {
       if (xwide_enabled()) xf_launch_cfg<NN, T, 1>(a, phys, dst, tw, s);
       else xf_launch_cfg<NN, T, 0>(a, phys, dst, tw, s);
     } else {
@@ -371,27 +371,30 @@ __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
   atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
 }
 
-// One wave per (y,x) row; a block holds ZW rows and each wave owns one LDS row buffer, so there is
+// One wave per (y,x) row; a block holds ZWT rows and each wave owns one LDS row buffer, so there is
 // no block barrier between the gather, the five FFTs, the product and the extraction.  The six
 // physical fields stay in registers (each lane owns points n = lane + 64 i of the row).
 constexpr int ZW = 4;
+// rows per block: fp64 at 2048 points takes 2 (4 row buffers + twiddles would exceed the LDS)
+template <int NZP, typename T>
+constexpr int zphys_rows() { return (sizeof(T) == 8 && NZP >= 2048) ? 2 : ZW; }
 
-template <int NZP, typename T, bool SEG>
-__global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
-                                                    const typename C2<T>::type* tw) {
+template <int NZP, typename T, bool SEG, int ZWT = zphys_rows<NZP, T>()>
+__global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+                                                         const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int PITCH = FftPitch<NZP>::value;
   constexpr int EP = (NZP + 63) / 64;  // points per lane
-  __shared__ T2 s[ZW * PITCH];
+  __shared__ T2 s[ZWT * PITCH];
   constexpr int TS = FftPlan<NZP>::TSIZE;
   __shared__ T2 tws[TS];  // twiddles staged once per block: LDS latency instead of L2 in the passes
-  __shared__ float red[4][ZW];
+  __shared__ float red[4][ZWT];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < TS; i += ZW * 64) tws[i] = tw[i];
+  for (int i = tid; i < TS; i += ZWT * 64) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
-  const long long r = static_cast<long long>(blockIdx.x) * ZW + w;
+  const long long r = static_cast<long long>(blockIdx.x) * ZWT + w;
   const int Kz = a.nkz - 1, nkz = a.nkz;
   const long long fs = a.field_stride;
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
@@ -529,7 +532,7 @@ __global__ void __launch_bounds__(256) zphys_kernel(ZArgs a, typename C2<T>::typ
   __syncthreads();
   if (tid < 4 && a.maxima) {
     float m = 0.f;
-    for (int i = 0; i < ZW; ++i) m = fmaxf(m, red[tid][i]);
+    for (int i = 0; i < ZWT; ++i) m = fmaxf(m, red[tid][i]);
     atomic_max_pos(&a.maxima[tid], m);
   }
 }
@@ -806,18 +809,15 @@ template <typename T>
 static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(a.Nzp, {
-    if constexpr (sizeof(T) == 8 && NN > 1024) {
-      CH_CHECK(false, "fp64 storage supports 2NZ-2 <= 1024");
-    } else {
-      const long long nrows = static_cast<long long>(a.ny) * a.NX;
-      dim3 grid(static_cast<unsigned>((nrows + ZW - 1) / ZW));
-      if (a.nseg > 1)
-        hipLaunchKernelGGL((zphys_kernel<NN, T, true>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
-                           static_cast<const T2*>(tw.buf));
-      else
-        hipLaunchKernelGGL((zphys_kernel<NN, T, false>), grid, dim3(256), 0, s, a, static_cast<T2*>(fields),
-                           static_cast<const T2*>(tw.buf));
-    }
+    constexpr int ZR = zphys_rows<NN, T>();
+    const long long nrows = static_cast<long long>(a.ny) * a.NX;
+    dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
+    if (a.nseg > 1)
+      hipLaunchKernelGGL((zphys_kernel<NN, T, true>), grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields),
+                         static_cast<const T2*>(tw.buf));
+    else
+      hipLaunchKernelGGL((zphys_kernel<NN, T, false>), grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields),
+                         static_cast<const T2*>(tw.buf));
   });
   HIP_LAUNCH_CHECK(s);
 }
@@ -882,17 +882,13 @@ template <typename T>
 static void fft_test_launch(void* data, int n, int batch, int dir, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   CH_DISPATCH_N(n, {
-    if constexpr (sizeof(T) == 8 && NN > 1024) {
-      CH_CHECK(false, "fp64 test FFT supports n <= 1024");
-    } else {
-      dim3 grid((batch + 3) / 4);
-      if (dir > 0)
-        hipLaunchKernelGGL((fft_test_kernel<NN, T, true>), grid, dim3(256), 0, s, static_cast<T2*>(data), batch,
-                           static_cast<const T2*>(tw.buf));
-      else
-        hipLaunchKernelGGL((fft_test_kernel<NN, T, false>), grid, dim3(256), 0, s, static_cast<T2*>(data), batch,
-                           static_cast<const T2*>(tw.buf));
-    }
+    dim3 grid((batch + 3) / 4);
+    if (dir > 0)
+      hipLaunchKernelGGL((fft_test_kernel<NN, T, true>), grid, dim3(256), 0, s, static_cast<T2*>(data), batch,
+                         static_cast<const T2*>(tw.buf));
+    else
+      hipLaunchKernelGGL((fft_test_kernel<NN, T, false>), grid, dim3(256), 0, s, static_cast<T2*>(data), batch,
+                         static_cast<const T2*>(tw.buf));
   });
   HIP_LAUNCH_CHECK(s);
 }

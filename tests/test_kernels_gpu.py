@@ -46,8 +46,6 @@ def test_yline_operators(native, NY, dtype):
 @pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_fft_c2c(native, n, dtype):
-    if dtype == torch.complex128 and n > 1024:
-        pytest.skip("fp64 test FFT limited to 1024")
     rng = np.random.default_rng(n)
     x = rng.standard_normal((7, n)) + 1j * rng.standard_normal((7, n))
     xt = torch.tensor(x, dtype=dtype, device=DEV)
@@ -58,7 +56,7 @@ def test_fft_c2c(native, n, dtype):
     assert rel(fwd, np.fft.fft(x, axis=-1)) < tol * np.log2(n)
 
 
-@pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20)])
+@pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20), (2048, 9)])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_xfft(native, NX, nkz, dtype):
     rng = np.random.default_rng(NX)
@@ -80,7 +78,8 @@ def test_xfft(native, NX, nkz, dtype):
 
 @pytest.mark.parametrize("NX,Nzp,dtype", [(32, 32, torch.complex128), (64, 128, torch.complex64),
                                           (16, 1024, torch.complex64), (16, 1024, torch.complex128),
-                                          (32, 2048, torch.complex64), (16, 512, torch.complex128)])
+                                          (32, 2048, torch.complex64), (8, 2048, torch.complex128),
+                                          (16, 512, torch.complex128)])
 def test_zphys(native, NX, Nzp, dtype):
     """z stage vs NumPy (LDS-pass kernel; the register-resident one is covered in a subprocess)."""
     rng = np.random.default_rng(Nzp)
