@@ -302,17 +302,32 @@ def test_reference_parity_modes_match_oracle(native, explicit_d2, influence, NX,
 
 
 def test_fp64_2048_point_transforms_run(native):
-    """fp64 storage at 2048-point x and z transforms (Re_tau~2000 on 8 GPUs in fp64):
-    a few steps run healthy and agree with the fp32 run of the same state to fp32 accuracy."""
-    kw = dict(NX=2048, NY=33, NZ=1025, Re=2000.0, ic="random", ic_amplitude=0.02, stats_every=0, log_every=0,
-              symmetry_every=0, dt_fixed=1e-4)
+    """fp64 storage at 2048-point x and z transforms (Re_tau~2000 on 8 GPUs in fp64).
+
+    The seeded IC is band-limited (exp(-k^2/32) envelope) and does not depend on the grid, so after
+    two steps the 2048 x 2048 run must agree with the (oracle-tested) 1024 x 1024 run on every mode
+    the smaller grid retains, and hold only round-off noise above it.  (An fp32-vs-fp64 comparison
+    is no use here: at NY = 33 the wall influence correction amplifies fp32 round-off in the
+    nonlinear term of the unresolved high modes by ~1e8; fp64 keeps it at ~1e-8.)"""
+    kw = dict(NY=33, Re=2000.0, ic="random", ic_amplitude=0.02, stats_every=0, log_every=0,
+              symmetry_every=0, dt_fixed=1e-4, precision="fp64")
     res = []
-    for prec in ("fp64", "fp32"):
-        s = make_solver(native, precision=prec, **kw)
+    for NX, NZ in ((2048, 1025), (1024, 513)):
+        s = make_solver(native, NX=NX, NZ=NZ, **kw)
         s.init_ic()
         s.prepare()
         for _ in range(2):
             s.step(False)
         assert s.health() == 0
         res.append(s.get_state())
-    assert rel(res[1][0], res[0][0]) < 1e-4 and rel(res[1][1], res[0][1]) < 1e-4
+        del s
+    big, small = res
+    nkx1, nkz1 = small[0].shape[1], small[0].shape[2]
+    nkx2 = big[0].shape[1]
+    kx1 = (nkx1 - 1) // 2
+    idx = np.r_[0:kx1 + 1, nkx2 - kx1:nkx2]
+    for f in range(2):
+        sub = big[f][:, idx, :nkz1]
+        assert rel(sub, small[f]) < 1e-7, f"field {f}"  # the ~1e-8 noise floor of the high modes
+        rest = np.linalg.norm(big[f]) ** 2 - np.linalg.norm(sub) ** 2
+        assert math.sqrt(max(rest, 0.0)) < 1e-6 * np.linalg.norm(sub), f"field {f} high modes"
