@@ -6,7 +6,7 @@
 //   1. each lane eliminates its R-1 interior rows (Thomas, fp64), expressing them through the
 //      separator rows of its own and its left neighbour (the lane's last row is a separator);
 //   2. the 64 separator unknowns form a tridiagonal system across lanes, solved by parallel cyclic
-//      reduction (6 levels of cross-lane exchange, ds_bpermute);
+//      reduction (6 levels of cross-lane exchange in the VALU: DPP and permlane swaps);
 //   3. each lane back-substitutes its interior rows.
 // The factorisation (elimination multipliers + PCR multipliers) is separated from the solve so
 // that several right-hand sides share one factorisation (complex data = 2 real RHS; the implicit
@@ -39,17 +39,103 @@ __device__ __forceinline__ double bperm(double v, int src_lane) {
 __device__ __forceinline__ float bperm(float v, int src_lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
 }
+
+// ---- cross-lane shifts in the VALU (no LDS) -------------------------------------------------
+// The solver's communication is fixed-stride shifts (PCR strides 1..32, halos, wave sums).  A
+// ds_bpermute is an LDS round trip (~100+ cycles) on the dependent chain of every PCR level and,
+// at one wave per SIMD, nothing hides it; it also competes with the staging tiles for LDS.  Here:
+//   stride 1      DPP wave_shr:1 / wave_shl:1 (one VALU op per dword)
+//   stride 2, 4   chains of stride-1 DPP moves
+//   stride 8      DPP row_shr/row_shl inside 16-lane rows + row_ror fed through a 16-lane shift
+//   stride 16     v_permlane16_swap + v_permlane32_swap (CDNA4), both directions at once
+//   stride 32     v_permlane32_swap, both directions at once
+// XV = false selects the ds_bpermute versions (kernels that spill VGPRs keep them: see xl_valu()).
+constexpr int kDppRowShl = 0x100, kDppRowShr = 0x110, kDppRowRor = 0x120, kDppWaveShl1 = 0x130,
+              kDppWaveShr1 = 0x138;
+template <int CTRL>
+__device__ __forceinline__ int dpp_z(int v) {  // lanes whose source is out of range read 0
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
+}
+// f of lane-16 (0 in rows 0) and of lane+16 (0 in row 3)
+__device__ __forceinline__ void xl_updn16(int f, int& up, int& dn) {
+  const int row = __lane_id() >> 4;
+  // p = {[f0 f0 f2 f2], [f1 f1 f3 f3]} (rows), q = {[f0 f0 f1 f1], [f2 f2 f3 f3]}
+  const auto p = __builtin_amdgcn_permlane16_swap(f, f, false, false);
+  const auto q = __builtin_amdgcn_permlane32_swap(p[0], p[1], false, false);
+  up = row == 0 ? 0 : static_cast<int>(row == 3 ? p[0] : q[0]);
+  dn = row == 3 ? 0 : static_cast<int>(row == 0 ? p[1] : q[1]);
+}
+// v of lane-S (0 for lanes < S) and of lane+S (0 for lanes >= 64-S); S is a compile-time constant
+// after unrolling at every call site
+__device__ __forceinline__ void xl_updn(int v, int s, int& up, int& dn) {
+  const int lane = __lane_id(), l16 = lane & 15;
+  switch (s) {
+    case 1:
+      up = dpp_z<kDppWaveShr1>(v);
+      dn = dpp_z<kDppWaveShl1>(v);
+      break;
+    case 2:
+      up = dpp_z<kDppWaveShr1>(dpp_z<kDppWaveShr1>(v));
+      dn = dpp_z<kDppWaveShl1>(dpp_z<kDppWaveShl1>(v));
+      break;
+    case 4:
+      up = dpp_z<kDppWaveShr1>(dpp_z<kDppWaveShr1>(dpp_z<kDppWaveShr1>(dpp_z<kDppWaveShr1>(v))));
+      dn = dpp_z<kDppWaveShl1>(dpp_z<kDppWaveShl1>(dpp_z<kDppWaveShl1>(dpp_z<kDppWaveShl1>(v))));
+      break;
+    case 8: {
+      const int a = dpp_z<kDppRowShr + 8>(v), b = dpp_z<kDppRowShl + 8>(v), f = dpp_z<kDppRowRor + 8>(v);
+      int u16, d16;
+      xl_updn16(f, u16, d16);
+      up = l16 >= 8 ? a : u16;
+      dn = l16 < 8 ? b : d16;
+      break;
+    }
+    case 16:
+      xl_updn16(v, up, dn);
+      break;
+    default: {  // 32
+      const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // {[v0 v1 v0 v1], [v2 v3 v2 v3]}
+      up = lane >= 32 ? static_cast<int>(q[0]) : 0;
+      dn = lane < 32 ? static_cast<int>(q[1]) : 0;
+    }
+  }
+}
+template <bool XV>
+__device__ __forceinline__ void xl_updn(double v, int s, double& up, double& dn) {
+  if constexpr (!XV) {
+    const int lane = __lane_id();
+    const double u = bperm(v, (lane - s) & 63), d = bperm(v, (lane + s) & 63);
+    up = lane >= s ? u : 0.0;
+    dn = lane + s < 64 ? d : 0.0;
+  } else {
+    int ul, uh, dl, dh;
+    xl_updn(__double2loint(v), s, ul, dl);
+    xl_updn(__double2hiint(v), s, uh, dh);
+    up = __hiloint2double(uh, ul);
+    dn = __hiloint2double(dh, dl);
+  }
+}
 // value of lane-s (0 for lanes < s)
-template <typename V>
-__device__ __forceinline__ V shfl_up_z(V v, int s, int lane) {
-  V r = bperm(v, (lane - s) & 63);
-  return lane >= s ? r : V(0);
+template <bool XV>
+__device__ __forceinline__ double shfl_up_z(double v, int s, int lane) {
+  if constexpr (XV) {
+    if (s == 1)
+      return __hiloint2double(dpp_z<kDppWaveShr1>(__double2hiint(v)), dpp_z<kDppWaveShr1>(__double2loint(v)));
+  }
+  double up, dn;
+  xl_updn<XV>(v, s, up, dn);
+  return up;
 }
 // value of lane+s (0 for lanes >= 64-s)
-template <typename V>
-__device__ __forceinline__ V shfl_down_z(V v, int s, int lane) {
-  V r = bperm(v, (lane + s) & 63);
-  return lane + s < 64 ? r : V(0);
+template <bool XV>
+__device__ __forceinline__ double shfl_down_z(double v, int s, int lane) {
+  if constexpr (XV) {
+    if (s == 1)
+      return __hiloint2double(dpp_z<kDppWaveShl1>(__double2hiint(v)), dpp_z<kDppWaveShl1>(__double2loint(v)));
+  }
+  double up, dn;
+  xl_updn<XV>(v, s, up, dn);
+  return dn;
 }
 // 1/x to full double precision: hardware reciprocal estimate + two Newton steps (each doubles the
 // correct bits).  Replaces IEEE division (~10 dependent instructions incl. scale/fixup) on the
@@ -62,8 +148,33 @@ __device__ __forceinline__ double fast_rcp(double x) {
   return __builtin_fma(r, e, r);
 }
 
+// value of lane src_lane (wave-uniform) in every lane
+template <bool XV>
 __device__ __forceinline__ double bcast(double v, int src_lane) {
-  return bperm(v, src_lane);
+  if constexpr (!XV)
+    return bperm(v, src_lane);
+  else
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), src_lane),
+                            __builtin_amdgcn_readlane(__double2loint(v), src_lane));
+}
+
+// sum over the wave, bitwise identical in every lane: rotations inside 16-lane rows (each lane
+// pairs with a partner that forms the same sum), then the row pairs and halves via permlane swaps
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  return __hiloint2double(dpp_z<CTRL>(__double2hiint(v)), dpp_z<CTRL>(__double2loint(v)));
+}
+__device__ __forceinline__ double xl_swap16(double v) {  // value of lane ^ 16
+  const int row = __lane_id() >> 4;
+  const auto ph = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  const auto pl = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  return (row & 1) ? __hiloint2double(ph[0], pl[0]) : __hiloint2double(ph[1], pl[1]);
+}
+__device__ __forceinline__ double xl_swap32(double v) {  // value of lane ^ 32
+  const bool lo = __lane_id() < 32;
+  const auto qh = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  const auto ql = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  return lo ? __hiloint2double(qh[1], ql[1]) : __hiloint2double(qh[0], ql[0]);
 }
 
 // Per-row coefficient tables, lane-major: tab[r*64 + lane] is row j = lane*R + r.
@@ -142,7 +253,7 @@ struct CoefHelm {
 };
 
 // ---- factorisation -----------------------------------------------------------------------
-template <int R, class Coef>
+template <int R, bool XV, class Coef>
 __device__ void pfactor(PFac<R>& F, const Coef& coef, int lane) {
   double A, B, C;
   if constexpr (R == 1) {
@@ -181,8 +292,8 @@ __device__ void pfactor(PFac<R>& F, const Coef& coef, int lane) {
     coef.abc(R - 1, as, bs, cs);
     F.as = as;
     F.cs = cs;
-    const double L0n = shfl_down_z(L_first, 1, lane);
-    const double U0n = shfl_down_z(U_first, 1, lane);
+    const double L0n = shfl_down_z<XV>(L_first, 1, lane);
+    const double U0n = shfl_down_z<XV>(U_first, 1, lane);
     A = as * L_last;
     B = bs + as * U_last + cs * L0n;
     C = cs * U0n;
@@ -193,8 +304,10 @@ __device__ void pfactor(PFac<R>& F, const Coef& coef, int lane) {
     // each lane inverts its own pivot once and the neighbours receive 1/B (one reciprocal per
     // level instead of two divisions)
     const double iB = fast_rcp(B);
-    const double Am = shfl_up_z(A, s, lane), iBm = shfl_up_z(iB, s, lane), Cm = shfl_up_z(C, s, lane);
-    const double Ap = shfl_down_z(A, s, lane), iBp = shfl_down_z(iB, s, lane), Cp = shfl_down_z(C, s, lane);
+    double Am, iBm, Cm, Ap, iBp, Cp;
+    xl_updn<XV>(A, s, Am, Ap);
+    xl_updn<XV>(iB, s, iBm, iBp);
+    xl_updn<XV>(C, s, Cm, Cp);
     const bool hm = lane >= s, hp = lane + s < 64;
     const double k1 = hm ? A * iBm : 0.0;
     const double k2 = hp ? C * iBp : 0.0;
@@ -245,7 +358,7 @@ __device__ void pfac_load(PFac<R>& F, const double* __restrict__ in, int lane) {
 }
 
 // ---- solve K right-hand sides in place ----------------------------------------------------
-template <int R, int K, class Coef>
+template <int R, int K, bool XV, class Coef>
 __device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], int lane) {
   double D[K];
   if constexpr (R == 1) {
@@ -273,15 +386,15 @@ __device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], in
       }
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) D[k] = d[k][R - 1] - F.as * PL[k] - F.cs * shfl_down_z(P0[k], 1, lane);
+    for (int k = 0; k < K; ++k) D[k] = d[k][R - 1] - F.as * PL[k] - F.cs * shfl_down_z<XV>(P0[k], 1, lane);
   }
 #pragma unroll
   for (int t = 0; t < kPcrLevels; ++t) {
     const int s = 1 << t;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const double Dm = shfl_up_z(D[k], s, lane);
-      const double Dp = shfl_down_z(D[k], s, lane);
+      double Dm, Dp;
+      xl_updn<XV>(D[k], s, Dm, Dp);
       D[k] = D[k] - F.k1[t] * Dm - F.k2[t] * Dp;
     }
   }
@@ -291,7 +404,7 @@ __device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], in
     if constexpr (R == 1) {
       d[k][0] = y;
     } else {
-      const double yl = shfl_up_z(y, 1, lane);
+      const double yl = shfl_up_z<XV>(y, 1, lane);
       d[k][0] -= F.a0 * yl;
       d[k][R - 2] -= F.cR2 * y;
       // interior solve with the separator values known
@@ -313,31 +426,31 @@ __device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], in
 
 // ---- stencils ----------------------------------------------------------------------------
 // value at global row j (wave-uniform j); returns 0 if j out of range
-template <int R>
+template <int R, bool XV>
 __device__ __forceinline__ double row_value(const double (&x)[R], int j, int lane) {
   const int src = j / R, rr = j - src * R;
   double v = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (r == rr) v = x[r];
-  return bcast(v, src);
+  return bcast<XV>(v, src);
 }
 
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ __forceinline__ void halo(const double (&x)[K][R], double (&left)[K], double (&right)[K], int lane) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    left[k] = shfl_up_z(x[k][R - 1], 1, lane);
-    right[k] = shfl_down_z(x[k][0], 1, lane);
+    left[k] = shfl_up_z<XV>(x[k][R - 1], 1, lane);
+    right[k] = shfl_down_z<XV>(x[k][0], 1, lane);
   }
 }
 
 // out = tridiag(lo, c, up) * x with per-row tables (c may be null => mask)
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ void apply_tri(const double* __restrict__ lo, const double* __restrict__ cc, const double* __restrict__ up,
                           const double (&x)[K][R], double (&out)[K][R], int lane) {
   double L[K], Rt[K];
-  halo<R, K>(x, L, Rt, lane);
+  halo<R, K, XV>(x, L, Rt, lane);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const double a = tab(lo, r, lane), b = tab(cc, r, lane), c = tab(up, r, lane);
@@ -351,16 +464,16 @@ __device__ void apply_tri(const double* __restrict__ lo, const double* __restric
 }
 
 // D1 right-hand side B1 f (interior stencil + 3-point one-sided wall closures)
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][R], int lane) {
-  apply_tri<R, K>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane);
+  apply_tri<R, K, XV>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane);
   const int N = t.N;
   const int jN = N - 1, lN = jN / R, rN = jN - lN * R;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double f1 = row_value<R>(x[k], 1, lane), f2 = row_value<R>(x[k], 2, lane);
-    const double g1 = row_value<R>(x[k], N - 2, lane), g2 = row_value<R>(x[k], N - 3, lane);
-    const double f0 = row_value<R>(x[k], 0, lane), g0 = row_value<R>(x[k], N - 1, lane);
+    const double f1 = row_value<R, XV>(x[k], 1, lane), f2 = row_value<R, XV>(x[k], 2, lane);
+    const double g1 = row_value<R, XV>(x[k], N - 2, lane), g2 = row_value<R, XV>(x[k], N - 3, lane);
+    const double f0 = row_value<R, XV>(x[k], 0, lane), g0 = row_value<R, XV>(x[k], N - 1, lane);
     if (lane == 0) out[k][0] = t.w0[0] * f0 + t.w0[1] * f1 + t.w0[2] * f2;
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -368,19 +481,34 @@ __device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][
   }
 }
 
-template <int K>
+template <int K, bool XV>
 __device__ __forceinline__ void wave_sum_n(double (&v)[K]) {
+  if constexpr (!XV) {
 #pragma unroll
-  for (int s = 32; s >= 1; s >>= 1)
+    for (int s = 32; s >= 1; s >>= 1)
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] += bperm(v[k], (__lane_id() ^ s));
+      for (int k = 0; k < K; ++k) v[k] += bperm(v[k], (__lane_id() ^ s));
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppRowRor + 8>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppRowRor + 4>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppRowRor + 2>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += dpp_d<kDppRowRor + 1>(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += xl_swap16(v[k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] += xl_swap32(v[k]);
 }
 
-template <int R>
+template <int R, bool XV>
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) v += bperm(v, (__lane_id() ^ s));
-  return v;
+  double a[1] = {v};
+  wave_sum_n<1, XV>(a);
+  return a[0];
 }
 
 }  // namespace dev

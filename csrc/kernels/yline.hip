@@ -62,13 +62,24 @@ int yline_supported_R(int NY) {
     default: CH_CHECK(false, "unsupported R=" << R_); \
   }
 
+// Cross-lane exchanges go through the VALU (DPP / permlane swaps, yline_device.hpp) in the
+// instantiations that fit their registers.  The ones that spill VGPRs keep ds_bpermute: the VALU
+// variant of kspec_kernel<10, float> (48 spilled VGPRs) faulted on MI355X with a memory aperture
+// violation that was not root-caused, and the spill-free kernels are where the latency matters.
+template <int R, typename T, int PAR = 0>
+constexpr bool xl_valu() {
+  if (PAR != 0) return false;
+  return sizeof(T) == 4 ? (R <= 3 || (R >= 5 && R <= 7)) : (R <= 3 || R == 5);
+}
+
 // ------------------------------------------------------------------------------------------
 template <int R>
 __global__ void __launch_bounds__(64) d1_factor_kernel(YTab t, double* out) {
+  constexpr bool XV = true;  // one wave, no register pressure
   const int lane = __lane_id();
   PFac<R> F;
   CoefD1 cd{t, lane};
-  pfactor<R>(F, cd, lane);
+  pfactor<R, XV>(F, cd, lane);
   pfac_store<R>(F, out, lane);
 }
 
@@ -166,34 +177,34 @@ void YTablesDev::release() {
 }
 
 // ---- shared helpers for line kernels --------------------------------------------------------
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ void d1_apply(const YTab& t, double (&x)[K][R], int lane) {
   double rhs[K][R];
-  d1_rhs<R, K>(t, x, rhs, lane);
+  d1_rhs<R, K, XV>(t, x, rhs, lane);
   PFac<R> F;
   pfac_load<R>(F, t.d1fac, lane);
   CoefD1 cd{t, lane};
-  psolve<R, K>(F, cd, rhs, lane);
+  psolve<R, K, XV>(F, cd, rhs, lane);
 #pragma unroll
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int r = 0; r < R; ++r) x[k][r] = rhs[k][r];
 }
 
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ __forceinline__ void apply_M(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
-  apply_tri<R, K>(t.m_lo, t.mask, t.m_up, x, o, lane);
+  apply_tri<R, K, XV>(t.m_lo, t.mask, t.m_up, x, o, lane);
 }
-template <int R, int K>
+template <int R, int K, bool XV>
 __device__ __forceinline__ void apply_K(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
-  apply_tri<R, K>(t.k_lo, t.k_c, t.k_up, x, o, lane);
+  apply_tri<R, K, XV>(t.k_lo, t.k_c, t.k_up, x, o, lane);
 }
 
 // value of complex line at row j (wave-uniform), returned in re/im
-template <int R>
+template <int R, bool XV>
 __device__ __forceinline__ void row_cplx(const double (&x)[2][R], int j, int lane, double& re, double& im) {
-  re = row_value<R>(x[0], j, lane);
-  im = row_value<R>(x[1], j, lane);
+  re = row_value<R, XV>(x[0], j, lane);
+  im = row_value<R, XV>(x[1], j, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -202,6 +213,7 @@ template <int R, typename T>
 __global__ void __launch_bounds__(256) yline_test_kernel(YTab t, int op, const void* vin, void* vout, int lines,
                                                          const double* k2s, double c) {
   using T2 = typename Cplx<T>::type;
+  constexpr bool XV = xl_valu<R, T>();
   const T2* in = static_cast<const T2*>(vin);
   T2* out = static_cast<T2*>(vout);
   const int lane = __lane_id();
@@ -218,39 +230,39 @@ __global__ void __launch_bounds__(256) yline_test_kernel(YTab t, int op, const v
   }
   const double k2 = k2s ? k2s[line] : 0.0;
   if (op == YOP_D1) {
-    d1_apply<R, 2>(t, x, lane);
+    d1_apply<R, 2, XV>(t, x, lane);
   } else if (op == YOP_HELM) {
     double m[2][R];
-    apply_M<R, 2>(t, x, m, lane);
+    apply_M<R, 2, XV>(t, x, m, lane);
     PFac<R> F;
     CoefHelm ch{t, lane, k2};
-    pfactor<R>(F, ch, lane);
-    psolve<R, 2>(F, ch, m, lane);
+    pfactor<R, XV>(F, ch, lane);
+    psolve<R, 2, XV>(F, ch, m, lane);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
   } else if (op == YOP_IMPL) {
     double m[2][R];
-    apply_M<R, 2>(t, x, m, lane);
+    apply_M<R, 2, XV>(t, x, m, lane);
     PFac<R> F;
     CoefImpl ci{t, lane, 1.0 + c * k2, c};
-    pfactor<R>(F, ci, lane);
-    psolve<R, 2>(F, ci, m, lane);
+    pfactor<R, XV>(F, ci, lane);
+    psolve<R, 2, XV>(F, ci, m, lane);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
   } else if (op == YOP_MAPPLY) {
     double m[2][R];
-    apply_M<R, 2>(t, x, m, lane);
+    apply_M<R, 2, XV>(t, x, m, lane);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int r = 0; r < R; ++r) x[k][r] = m[k][r];
   } else if (op == YOP_KAPPLY) {
     double m[2][R];
-    apply_K<R, 2>(t, x, m, lane);
+    apply_K<R, 2, XV>(t, x, m, lane);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -399,6 +411,7 @@ __device__ __forceinline__ void chs_profiles(double l, double y, double& C, doub
 template <int R, typename T, int W, int PAR = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
+  constexpr bool XV = xl_valu<R, T, PAR>();
   // Coefficient tables (14 per-row tables + the D1 factorisation) are staged into LDS once per
   // block when they fit: every solve step reads them, and from L2 each read is a dependent
   // ~500-cycle load at one wave per SIMD.  Offsets are compile-time so the reads stay ds_read.
@@ -533,7 +546,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           G[1][r] -= al * H[0][r];
         }
       }
-      d1_apply<R, 2>(t, X, lane);  // D(-i al Hx - i be Hz)
+      d1_apply<R, 2, XV>(t, X, lane);  // D(-i al Hx - i be Hz)
       {
         double Hy[2][R];
         st.template commit<2>(Hy);
@@ -542,8 +555,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #pragma unroll
           for (int r = 0; r < R; ++r) X[k][r] -= k2 * Hy[k][r];
       }
-      apply_M<R, 2>(t, X, RPn, lane);
-      apply_M<R, 2>(t, G, RWn, lane);
+      apply_M<R, 2, XV>(t, X, RPn, lane);
+      apply_M<R, 2, XV>(t, G, RWn, lane);
       KSPEC_STAMP(0)
       if (a.mean_diag && is_mean) {
 #pragma unroll
@@ -566,16 +579,16 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
             for (int k = 0; k < 2; ++k)
 #pragma unroll
               for (int r = 0; r < R; ++r) DD[k][r] = qq[k][r];
-            d1_apply<R, 2>(t, DD, lane);
-            d1_apply<R, 2>(t, DD, lane);
-            apply_M<R, 2>(t, DD, Kq, lane);
+            d1_apply<R, 2, XV>(t, DD, lane);
+            d1_apply<R, 2, XV>(t, DD, lane);
+            apply_M<R, 2, XV>(t, DD, Kq, lane);
             return;
           }
         }
-        apply_K<R, 2>(t, qq, Kq, lane);
+        apply_K<R, 2, XV>(t, qq, Kq, lane);
       };
       st.template commit<3>(q);  // phi
-      apply_M<R, 2>(t, q, Mq, lane);
+      apply_M<R, 2, XV>(t, q, Mq, lane);
       explicit_d2(q);
 #pragma unroll
       for (int k = 0; k < 2; ++k)
@@ -583,7 +596,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         for (int r = 0; r < R; ++r)
           rhsP[k][r] = Mq[k][r] + dt * (a.rk_a * a.nu * (Kq[k][r] - k2 * Mq[k][r]) + a.rk_g * RPn[k][r]);
       st.template commit<4>(q);  // omega
-      apply_M<R, 2>(t, q, Mq, lane);
+      apply_M<R, 2, XV>(t, q, Mq, lane);
       explicit_d2(q);
 #pragma unroll
       for (int k = 0; k < 2; ++k)
@@ -615,7 +628,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     {
       PFac<R> F;
       CoefImpl ci{t, lane, 1.0 + c * k2, c};
-      pfactor<R>(F, ci, lane);
+      pfactor<R, XV>(F, ci, lane);
       {
         // omega, phi and the two homogeneous phi solutions share the factorisation: one solve
         // with 6 real right-hand sides keeps 6 independent chains in flight per PCR level
@@ -630,7 +643,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           Z[4][r] = (j == 0) ? 1.0 : 0.0;
           Z[5][r] = (j == N - 1) ? 1.0 : 0.0;
         }
-        psolve<R, 6>(F, ci, Z, lane);
+        psolve<R, 6, XV>(F, ci, Z, lane);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           rhsW[0][r] = Z[0][r];
@@ -643,7 +656,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       if (is_mean) {
         // constant flow rate: U += C * U1, U1 = response to a unit mean pressure gradient
-        const double fU = wave_sum<R>([&] {
+        const double fU = wave_sum<R, XV>([&] {
           double s = 0;
 #pragma unroll
           for (int r = 0; r < R; ++r) s += tab(t.trap, r, lane) * rhsW[0][r];
@@ -653,11 +666,11 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           double U1[1][R], one[1][R], M1[1][R];
 #pragma unroll
           for (int r = 0; r < R; ++r) one[0][r] = (lane * R + r < N) ? 1.0 : 0.0;
-          apply_tri<R, 1>(t.m_lo, t.mask, t.m_up, one, M1, lane);
+          apply_tri<R, 1, XV>(t.m_lo, t.mask, t.m_up, one, M1, lane);
 #pragma unroll
           for (int r = 0; r < R; ++r) U1[0][r] = M1[0][r];
-          psolve<R, 1>(F, ci, U1, lane);
-          const double f1 = wave_sum<R>([&] {
+          psolve<R, 1, XV>(F, ci, U1, lane);
+          const double f1 = wave_sum<R, XV>([&] {
             double s = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) s += tab(t.trap, r, lane) * U1[0][r];
@@ -686,7 +699,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     {
       PFac<R> F;
       CoefHelm chm{t, lane, k2};
-      pfactor<R>(F, chm, lane);
+      pfactor<R, XV>(F, chm, lane);
       double vH[2][R];
       {
         double Y[4][R], Z[4][R];
@@ -697,8 +710,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           Z[2][r] = phH[0][r];
           Z[3][r] = phH[1][r];
         }
-        apply_M<R, 4>(t, Z, Y, lane);
-        psolve<R, 4>(F, chm, Y, lane);
+        apply_M<R, 4, XV>(t, Z, Y, lane);
+        psolve<R, 4, XV>(F, chm, Y, lane);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           v[0][r] = Y[0][r];
@@ -721,7 +734,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         acc[6] += g0 * vH[1][r];
         acc[7] += gN * vH[1][r];
       }
-      wave_sum_n<8>(acc);
+      wave_sum_n<8, XV>(acc);
       const double p0r = acc[0], p0i = acc[1], pNr = acc[2], pNi = acc[3];
       double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
       if constexpr ((PAR & kParAnalytic) != 0) {
@@ -789,9 +802,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     st.load(omega, om);
     PFac<R> F;
     CoefHelm chm{t, lane, k2};
-    pfactor<R>(F, chm, lane);
-    apply_M<R, 2>(t, ph, v, lane);
-    psolve<R, 2>(F, chm, v, lane);
+    pfactor<R, XV>(F, chm, lane);
+    apply_M<R, 2, XV>(t, ph, v, lane);
+    psolve<R, 2, XV>(F, chm, v, lane);
     if (is_mean || k2 == 0.0) {
       czero<R>(ph);
       czero<R>(v);
@@ -818,7 +831,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       Z[2][r] = om[0][r];
       Z[3][r] = om[1][r];
     }
-    d1_apply<R, 4>(t, Z, lane);
+    d1_apply<R, 4, XV>(t, Z, lane);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       dv[0][r] = Z[0][r];
@@ -910,7 +923,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     st.store(out[5], wz);
   }
   if (a.mean_diag && is_mean) {
-    const double d0 = row_value<R>(Dom[0], 0, lane), dN = row_value<R>(Dom[0], N - 1, lane);
+    const double d0 = row_value<R, XV>(Dom[0], 0, lane), dN = row_value<R, XV>(Dom[0], N - 1, lane);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int j = lane * R + r;
