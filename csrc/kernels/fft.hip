@@ -118,7 +118,9 @@ __device__ __forceinline__ SegPos seg_find(const int* start, const long long* of
 // into registers right after the current tile is staged into LDS, so they are in flight during
 // the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
-template <int NX, typename T, bool SEG, int WIDE>
+// ONE: a single source block without a self block (one rank): plain [y][kx][kz] addressing, no
+// segment lookup (22 unrolled 8-way compare/select chains per tile otherwise)
+template <int NX, typename T, bool SEG, int WIDE, bool ONE = false>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -151,10 +153,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
       // columns kz >= nkz are transformed (independently) but never stored
       const int i = min(e / C, a.nkx - 1);
       const int kz = min(kz0 + e % C, a.nkz - 1);
-      const SegPos sp = seg_find(src.kx_start, src.off, src.nsrc, i);
-      const T2* b = sp.idx == src.self_seg ? sbase : base;
-      // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
-      v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
+      if constexpr (ONE) {
+        v[q] = base[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      } else {
+        const SegPos sp = seg_find(src.kx_start, src.off, src.nsrc, i);
+        const T2* b = sp.idx == src.self_seg ? sbase : base;
+        // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
+        v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
+      }
     }
   };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
@@ -201,7 +207,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
   }
 }
 
-template <int NX, typename T, bool SEG, int WIDE>
+template <int NX, typename T, bool SEG, int WIDE, bool ONE = false>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -265,9 +271,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
       const int kz = kz0 + c;
       if (kz < a.nkz) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
-        const SegPos sp = seg_find(dst.kx_start, dst.off, dst.ndst, i);
-        T2* ob = sp.idx == dst.self_seg ? soutb : outb;
-        ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        if constexpr (ONE) {
+          outb[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
+              s[c * PITCH + fft_pidx(x)];
+        } else {
+          const SegPos sp = seg_find(dst.kx_start, dst.off, dst.ndst, i);
+          T2* ob = sp.idx == dst.self_seg ? soutb : outb;
+          ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        }
       }
     }
   }
@@ -290,7 +301,9 @@ template <int NN, typename T, int WIDE>
 static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true, WIDE> : xfft_backward_kernel<NN, T, false, WIDE>;
+  const bool one = src.nsrc == 1 && src.self_seg < 0 && src.off[0] == 0;
+  auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true, WIDE>
+                          : (one ? xfft_backward_kernel<NN, T, false, WIDE, true> : xfft_backward_kernel<NN, T, false, WIDE>);
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
@@ -300,7 +313,9 @@ template <int NN, typename T, int WIDE>
 static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true, WIDE> : xfft_forward_kernel<NN, T, false, WIDE>;
+  const bool one = dst.ndst == 1 && dst.self_seg < 0 && dst.off[0] == 0;
+  auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true, WIDE>
+                          : (one ? xfft_forward_kernel<NN, T, false, WIDE, true> : xfft_forward_kernel<NN, T, false, WIDE>);
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
@@ -362,6 +377,7 @@ void xfft_forward(const XArgs& a_in, const void* phys, const XDst& dst, const Tw
   const XArgs a = norm_pseg(a_in);
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_forward: twiddle table mismatch");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_forward: per-field plane block exceeds 32-bit offsets");
+  CH_CHECK(static_cast<long long>(a.ny) * a.nkx * a.nkz < (1LL << 32), "xfft_forward: per-field spectral block exceeds 32-bit offsets");
   if (fp64) xf_launch<double>(a, phys, dst, tw, s);
   else xf_launch<float>(a, phys, dst, tw, s);
 }
@@ -410,14 +426,10 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
 
   if (r < nrows) {  // wave-uniform
     T2 ph[3][EP];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
-      // (a real z-row has a real mean), zero padding between Kz and N-Kz.
+    constexpr int MK = (NZP / 2 + 63) / 64;
+    auto fetch = [&](int p, T2 (&va)[MK], T2 (&vb)[MK]) {
       const T2* A = fields + (2 * p) * fs;
       const T2* B = fields + (2 * p + 1) * fs;
-      constexpr int MK = (NZP / 2 + 63) / 64;
-      T2 va[MK], vb[MK];
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
         const int k = lane + 64 * i;
@@ -425,6 +437,34 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
         va[i] = k < nkz ? A[o] : T2{0, 0};
         vb[i] = k < nkz ? B[o] : T2{0, 0};
       }
+    };
+    // the next pair's loads are in flight during each transform where the 24 registers fit (fp32,
+    // <= 1024 points, one segment); elsewhere each pair is loaded right before its transform
+    constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
+    T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
+    if constexpr (kPrefetch) fetch(0, pa, pb);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      T2 va[MK], vb[MK];
+      if constexpr (kPrefetch) {
+#pragma unroll
+        for (int i = 0; i < MK; ++i) {
+          va[i] = pa[i];
+          vb[i] = pb[i];
+        }
+      } else {
+        const T2* A = fields + (2 * p) * fs;
+        const T2* B = fields + (2 * p + 1) * fs;
+#pragma unroll
+        for (int i = 0; i < MK; ++i) {
+          const int k = lane + 64 * i;
+          const long long o = k < nkz ? zaddr(k) : 0;
+          va[i] = k < nkz ? A[o] : T2{0, 0};
+          vb[i] = k < nkz ? B[o] : T2{0, 0};
+        }
+      }
+      // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
+      // (a real z-row has a real mean), zero padding between Kz and N-Kz.
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
         const int k = lane + 64 * i;
@@ -438,6 +478,9 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
         }
       }
       for (int k = Kz + 1 + lane; k < NZP - Kz; k += 64) row[fft_pidx(k)] = T2{0, 0};
+      if constexpr (kPrefetch) {
+        if (p < 2) fetch(p + 1, pa, pb);
+      }
       __builtin_amdgcn_wave_barrier();
       if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, true>(row, tws, lane);
 #pragma unroll
