@@ -113,14 +113,34 @@ __device__ __forceinline__ SegPos seg_find(const int* start, const long long* of
   return p;
 }
 
+// Segment of i for i in the wave-uniform window [lo, lo + span) when every segment is at least
+// span long (checked on the host): the window meets at most two segments, found with scalar
+// lookups of its two ends, and each lane picks one with a single compare.
+template <int MAXS = 8>
+__device__ __forceinline__ SegPos seg_find_win(const int* start, const long long* off, int n, int lo, int span, int i) {
+  const SegPos a = seg_find<MAXS>(start, off, n, lo);
+  const SegPos b = seg_find<MAXS>(start, off, n, lo + span - 1);
+  return i >= b.start ? b : a;
+}
+// kx segment addressing of the x kernels: kSegOne = one block, no self block (one rank);
+// kSegWin = window lookup (seg_find_win); kSegFull = per-element lookup
+constexpr int kSegOne = 0, kSegWin = 1, kSegFull = 2;
+template <int NT, int C>
+inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
+  if (n == 1 && self_seg < 0 && off0 == 0) return kSegOne;
+  int m = 1 << 30;
+  for (int q = 0; q < n; ++q) m = std::min(m, start[q + 1] - start[q]);
+  return m >= NT / C ? kSegWin : kSegFull;
+}
+
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
 // LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
 // into registers right after the current tile is staged into LDS, so they are in flight during
 // the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
-// ONE: a single source block without a self block (one rank): plain [y][kx][kz] addressing, no
-// segment lookup (22 unrolled 8-way compare/select chains per tile otherwise)
-template <int NX, typename T, bool SEG, int WIDE, bool ONE = false>
+// SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
+// compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -153,10 +173,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
       // columns kz >= nkz are transformed (independently) but never stored
       const int i = min(e / C, a.nkx - 1);
       const int kz = min(kz0 + e % C, a.nkz - 1);
-      if constexpr (ONE) {
+      if constexpr (SM == kSegOne) {
         v[q] = base[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
       } else {
-        const SegPos sp = seg_find(src.kx_start, src.off, src.nsrc, i);
+        const SegPos sp = SM == kSegWin ? seg_find_win(src.kx_start, src.off, src.nsrc, (q * NT) / C, NT / C, i)
+                                        : seg_find(src.kx_start, src.off, src.nsrc, i);
         const T2* b = sp.idx == src.self_seg ? sbase : base;
         // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
         v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
@@ -207,7 +228,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
   }
 }
 
-template <int NX, typename T, bool SEG, int WIDE, bool ONE = false>
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -266,16 +287,18 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
     // this rank's own block goes straight into its spectral field (no self exchange)
     T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
-    for (int e = tid; e < a.nkx * C; e += NT) {
+    for (int e0 = 0; e0 < a.nkx * C; e0 += NT) {
+      const int e = e0 + tid;
       const int i = e / C, c = e - i * C;
       const int kz = kz0 + c;
-      if (kz < a.nkz) {
+      if (e < a.nkx * C && kz < a.nkz) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
-        if constexpr (ONE) {
+        if constexpr (SM == kSegOne) {
           outb[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
               s[c * PITCH + fft_pidx(x)];
         } else {
-          const SegPos sp = seg_find(dst.kx_start, dst.off, dst.ndst, i);
+          const SegPos sp = SM == kSegWin ? seg_find_win(dst.kx_start, dst.off, dst.ndst, e0 / C, NT / C, i)
+                                          : seg_find(dst.kx_start, dst.off, dst.ndst, i);
           T2* ob = sp.idx == dst.self_seg ? soutb : outb;
           ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
         }
@@ -301,9 +324,12 @@ template <int NN, typename T, int WIDE>
 static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  const bool one = src.nsrc == 1 && src.self_seg < 0 && src.off[0] == 0;
-  auto kern = a.npseg > 1 ? xfft_backward_kernel<NN, T, true, WIDE>
-                          : (one ? xfft_backward_kernel<NN, T, false, WIDE, true> : xfft_backward_kernel<NN, T, false, WIDE>);
+  // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
+  // its windows, computed up front, spilled ~640 SGPRs)
+  const int sm = seg_mode<Cfg::NT, Cfg::C>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
+  auto kern = a.npseg > 1     ? xfft_backward_kernel<NN, T, true, WIDE>
+              : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne>
+                              : xfft_backward_kernel<NN, T, false, WIDE, kSegFull>;
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
@@ -313,9 +339,11 @@ template <int NN, typename T, int WIDE>
 static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  const bool one = dst.ndst == 1 && dst.self_seg < 0 && dst.off[0] == 0;
-  auto kern = a.npseg > 1 ? xfft_forward_kernel<NN, T, true, WIDE>
-                          : (one ? xfft_forward_kernel<NN, T, false, WIDE, true> : xfft_forward_kernel<NN, T, false, WIDE>);
+  const int sm = seg_mode<Cfg::NT, Cfg::C>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
+  auto kern = a.npseg > 1             ? xfft_forward_kernel<NN, T, true, WIDE>
+              : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne>
+              : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin>
+                              : xfft_forward_kernel<NN, T, false, WIDE, kSegFull>;
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
