@@ -40,10 +40,61 @@ template <typename T2>
 __device__ __forceinline__ T2 csub(T2 a, T2 b) {
   return T2{a.x - b.x, a.y - b.y};
 }
+// fp32: the same operations on the native 2-vector, so each complex add/sub is one v_pk_add_f32
+// and a complex product one v_pk_mul_f32 + one v_pk_fma_f32 with operand swizzles (component-wise
+// code left the pairing to the SLP vectoriser, which built its pairs with v_mov shuffles)
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v_t v2(float2 a) { return __builtin_bit_cast(f2v_t, a); }
+__device__ __forceinline__ float2 c2v(f2v_t a) { return __builtin_bit_cast(float2, a); }
+template <>
+__device__ __forceinline__ float2 cadd<float2>(float2 a, float2 b) {
+  return c2v(v2(a) + v2(b));
+}
+template <>
+__device__ __forceinline__ float2 csub<float2>(float2 a, float2 b) {
+  return c2v(v2(a) - v2(b));
+}
+template <>
+__device__ __forceinline__ float2 cmul<float2>(float2 a, float2 b) {
+  const f2v_t x = v2(a), y = v2(b);
+  const f2v_t yr = {-y.y, y.x};
+  return c2v(__builtin_elementwise_fma(x.yy, yr, x.xx * y));
+}
+
+// complex product by a twiddle loaded at run time: fp32 as v_pk_mul_f32 + v_pk_fma_f32 with the
+// broadcasts and the swap in op_sel / op_sel_hi (the compiler built those operand pairs with two
+// v_mov_b32 each)
+template <bool CONJ, typename T2>
+__device__ __forceinline__ T2 cmul_tw(T2 a, T2 b) {  // a * b, or a * conj(b)
+  if constexpr (sizeof(T2) == 8) {
+    const f2v_t x = v2(a), y = v2(b);
+    f2v_t t, r;
+    if constexpr (!CONJ) {
+      // t = (ax*bx, ax*by); r = (-ay*by + t.x, ay*bx + t.y)
+      asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(x), "v"(y));
+      asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+          : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    } else {
+      // t = (ax*bx, -ax*by); r = (ay*by + t.x, ay*bx + t.y)
+      asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(x), "v"(y));
+      asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(x), "v"(y), "v"(t));
+    }
+    return c2v(r);
+  } else {
+    if constexpr (CONJ) b.y = -b.y;
+    return cmul(a, b);
+  }
+}
+
 // multiply by -i (forward) or +i (inverse)
 template <bool INV, typename T2>
 __device__ __forceinline__ T2 mul_mi(T2 d) {
-  return INV ? T2{-d.y, d.x} : T2{d.y, -d.x};
+  if constexpr (sizeof(T2) == 8) {  // float2: a swizzle + sign the packed adds can absorb
+    const f2v_t v = v2(d);
+    return c2v(INV ? f2v_t{-v.y, v.x} : f2v_t{v.y, -v.x});
+  } else {
+    return INV ? T2{-d.y, d.x} : T2{d.y, -d.x};
+  }
 }
 
 constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
@@ -219,9 +270,7 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       if constexpr (NS > 1) {
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          T2 w = tw[(r - 1) * NS + k];
-          if (INV) w.y = -w.y;
-          v[b][r] = cmul(v[b][r], w);
+          v[b][r] = cmul_tw<INV>(v[b][r], tw[(r - 1) * NS + k]);
         }
       }
       dftR<R, INV>(v[b]);
