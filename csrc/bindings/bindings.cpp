@@ -66,6 +66,17 @@ struct YLineOps {
     yline_test(tab, op, in.data_ptr(), out.data_ptr(), lines, k2p, c, f64, cur_stream());
     return out;
   }
+  // the dense-D1 MFMA kernel (complex128 only)
+  DenseD1Dev dense;
+  torch::Tensor d1_mfma(torch::Tensor in) {
+    check_dev_tensor(in, "in");
+    TORCH_CHECK(is_fp64_complex(in), "d1_mfma: complex128 input");
+    TORCH_CHECK(in.dim() == 2 && in.size(0) == grid.N, "in must be [NY, lines]");
+    if (!dense.d) dense.upload(grid, cur_stream());
+    auto out = torch::zeros_like(in);
+    d1_dense_mfma(dense, in.data_ptr(), out.data_ptr(), static_cast<int>(in.size(1)), cur_stream());
+    return out;
+  }
 };
 
 std::map<std::pair<int, bool>, std::unique_ptr<Twiddles>>& tw_cache() {
@@ -184,7 +195,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   py::class_<YLineOps>(m, "YLineOps")
       .def(py::init<int, double>(), py::arg("NY"), py::arg("stretch") = 2.0)
-      .def("apply", &YLineOps::apply, py::arg("op"), py::arg("x"), py::arg("k2") = py::none(), py::arg("c") = 0.0);
+      .def("apply", &YLineOps::apply, py::arg("op"), py::arg("x"), py::arg("k2") = py::none(), py::arg("c") = 0.0)
+      .def("d1_mfma", &YLineOps::d1_mfma, py::arg("x"));
 
   m.def("fft_c2c", &fft_c2c, "batched in-LDS C2C FFT along the last axis; dir=+1 inverse (unnormalised)");
   m.def("xfft_backward", &xfft_b);

@@ -36,6 +36,17 @@ enum YLineOp : int {
 void yline_test(const YTablesDev& t, int op, const void* in, void* out, int lines, const double* k2, double c,
                 bool fp64, hipStream_t stream);
 
+// Dense D1 = A1^-1 B1 (NY <= 192) applied to [y][line] complex fp64 lines on the matrix cores
+// (yline_mfma.hip): the measured MFMA alternative to the PCR D1 solve.
+struct DenseD1Dev {
+  double* d = nullptr;  // [NP][NP] row-major, zero-padded
+  int N = 0, NP = 0;
+  void upload(const YGrid& g, hipStream_t stream);
+  void release();
+  ~DenseD1Dev() { release(); }
+};
+void d1_dense_mfma(const DenseD1Dev& m, const void* in, void* out, int lines, hipStream_t stream);
+
 // ---- the fused spectral (y-line) substep kernel ---------------------------------------------
 struct SpecArgs {
   // geometry

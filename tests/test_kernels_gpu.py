@@ -43,6 +43,18 @@ def test_yline_operators(native, NY, dtype):
         assert e < t, f"op {op} NY={NY} {dtype}: rel err {e:.3e}"
 
 
+@pytest.mark.parametrize("NY", [33, 65, 129, 192])
+def test_d1_dense_mfma(native, NY):
+    """Dense D1 on the matrix cores (v_mfma_f64_16x16x4_f64) against the dense NumPy D1."""
+    rng = np.random.default_rng(100 + NY)
+    L = 37  # not a multiple of the 8 lines per block
+    ops = ora.build_ops(NY)
+    x = rng.standard_normal((NY, L)) + 1j * rng.standard_normal((NY, L))
+    Y = native.YLineOps(NY)
+    got = Y.d1_mfma(torch.tensor(x, dtype=torch.complex128, device=DEV)).cpu().numpy()
+    assert rel(got, ora.op_d1(ops, x)) < 1e-10
+
+
 @pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_fft_c2c(native, n, dtype):
