@@ -65,7 +65,10 @@ int yline_supported_R(int NY) {
 // Cross-lane exchanges go through the VALU (DPP / permlane swaps, yline_device.hpp) in the
 // instantiations that fit their registers.  The ones that spill VGPRs keep ds_bpermute: the VALU
 // variant of kspec_kernel<10, float> (48 spilled VGPRs) faulted on MI355X with a memory aperture
-// violation that was not root-caused, and the spill-free kernels are where the latency matters.
+// violation, and so did a DPP-only variant (no permlane swaps) of kspec_kernel<10, double> (104
+// spilled VGPRs) while the DPP-only <10, float> passed its oracle test: the fault follows the
+// spilling kernels, not one instruction; not root-caused.  The spill-free kernels are the ones
+// where the exchange latency matters (one wave per SIMD, no spill traffic to hide it).
 template <int R, typename T, int PAR = 0>
 constexpr bool xl_valu() {
   if (PAR != 0) return false;
