@@ -309,8 +309,23 @@ struct SpecTile {
   // (128x129x128 fp64 1.18 -> 0.84 ms/step); register slots at R = 5..8 despite some spills
   // (1024x385x1024 fp64: 99.4 ms vs 105.7 ms address-only)
   static constexpr bool kRegSlots = R <= 2 || (R >= 5 && R <= 8);
-  T2* tile;
+  T2* tile;             // the buffer of the last staging (column() reads it)
   int N, lines, line0, w, lane;
+  // Double buffering (tile2 != nullptr): consecutive stagings alternate between two buffers, so a
+  // staging's writes cannot race the previous staging's cross-wave reads and only the barrier
+  // between its own writes and reads remains.  (Two stagings back, the buffer was freed by the
+  // intervening staging's barrier: every wave drains its LDS reads, lgkmcnt(0), before it.)
+  T2* tile2 = nullptr;
+  __device__ T2* next_tile() {
+    if (tile2) {
+      T2* t = tile2;
+      tile2 = tile;
+      tile = t;
+    } else {
+      lds_barrier();  // single buffer: the previous staging's reads must be done
+    }
+    return tile;
+  }
   T2 pend[kRegSlots ? NS : 1][R];  // prefetch slots: this thread's share of fields whose loads are in flight
   const T2* dsrc[kRegSlots ? 1 : NS];
   int dl0[kRegSlots ? 1 : NS];
@@ -337,8 +352,8 @@ struct SpecTile {
   }
   // Stage the prefetched field through the LDS tile and return this wave's line.
   template <int S = 0>
-  __device__ void commit(double (&x)[2][R]) const {
-    lds_barrier();
+  __device__ void commit(double (&x)[2][R]) {
+    next_tile();
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int e = threadIdx.x + q * W * 64;
@@ -373,8 +388,8 @@ struct SpecTile {
     prefetch(src);
     commit(x);
   }
-  __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) const {
-    lds_barrier();
+  __device__ void store(T2* __restrict__ dst, const double (&x)[2][R]) {
+    next_tile();
 #pragma unroll
     for (int r = 0; r < R; ++r) tile[r * PLANE + lane * PITCH + w] = T2{static_cast<T>(x[0][r]), static_cast<T>(x[1][r])};
     lds_barrier();
@@ -445,7 +460,12 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     t.d1fac = tab_lds + 14 * ROWS;
     __syncthreads();
   }
-  __shared__ T2 tile_mem[R * (64 * (W + 1) + 1)];
+  constexpr int TILE = R * (64 * (W + 1) + 1);
+  // a second staging buffer where it fits next to the tables at this kernel's blocks per CU
+  // (W = 8: two blocks per CU, W = 4: one)
+  constexpr int kLdsBudget = (W == 8 ? 78 : 150) * 1024;
+  constexpr bool kDoubleTile = (TLDS ? NTAB * 8 : 0) + 2 * TILE * static_cast<int>(sizeof(T2)) <= kLdsBudget;
+  __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * TILE];
   double* sred = reinterpret_cast<double*>(tile_mem);  // stats reduction reuses the staging tile
   static_assert(sizeof(T2) * (W + 1) >= 4 * sizeof(double), "tile too small for the stats reduction");
   const int lane = __lane_id();
@@ -459,6 +479,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   SpecTile<R, T, W, 7> st{tile_mem, N, a.lines, lb * W, w, lane};
+  if constexpr (kDoubleTile) st.tile2 = tile_mem + TILE;
   T2* phi = static_cast<T2*>(a.phi);
   T2* omega = static_cast<T2*>(a.omega);
   T2* Rphi = static_cast<T2*>(a.Rphi);
