@@ -237,6 +237,43 @@ inline void fft_twiddle_fill(int n, F&& put) {  // put(index, m): entry index ho
   if (r2 > 1) pass(r2, r0 * r1);
 }
 
+// ---- real-signal forward transform of the z stage (N = 1024, 2048) -------------------------
+// A real row x of length N is packed as z_m = x_2m + i x_2m+1 and transformed at length H = N/2;
+// X_k = E_k + W_N^k O_k with E_k = (Z_k + conj Z_{H-k})/2, O_k = (Z_k - conj Z_{H-k})/(2i).
+// Radices of the half transform: 512 = 8x8x8 and 1024 = 16x16x4, so every pass gives each of the
+// 64 lanes exactly one butterfly (a 16x16x2 plan of 512 would idle half the wave in two passes).
+// Its tables are appended to the N-point table: [post W_N^k, k < N/2][pass 2][pass 3].
+template <int N>
+struct HalfPlan {
+  static constexpr bool ok = N == 1024 || N == 2048;
+  static constexpr int H = N / 2;
+  static constexpr int R0 = H == 512 ? 8 : 16, R1 = R0, R2 = H / (R0 * R1);
+  static constexpr int POST = H;                    // post-processing twiddles W_N^k
+  static constexpr int P2 = POST;                   // offset of pass 2 (R1, NS = R0)
+  static constexpr int P3 = P2 + (R1 - 1) * R0;     // offset of pass 3 (R2, NS = R0*R1)
+  static constexpr int SIZE = ok ? P3 + (R2 - 1) * R0 * R1 : 0;
+};
+inline int fft_half_twiddle_size(int n) {
+  if (n != 1024 && n != 2048) return 0;
+  const int h = n / 2, r0 = h == 512 ? 8 : 16, r2 = h / (r0 * r0);
+  return h + (r0 - 1) * r0 + (r2 - 1) * r0 * r0;
+}
+template <typename F>
+inline void fft_half_twiddle_fill(int n, F&& put) {  // put(index, m): entry holds W_n^m
+  if (fft_half_twiddle_size(n) == 0) return;
+  const int h = n / 2, r0 = h == 512 ? 8 : 16, r2 = h / (r0 * r0);
+  for (int k = 0; k < h; ++k) put(k, k);
+  int off = h;
+  auto pass = [&](int R, int NS) {  // W_h^(k r h/(R NS)) = W_n^(2 k r h/(R NS))
+    const int stride = h / (R * NS);
+    for (int r = 1; r < R; ++r)
+      for (int k = 0; k < NS; ++k) put(off + (r - 1) * NS + k, 2 * k * r * stride);
+    off += (R - 1) * NS;
+  };
+  pass(r0, r0);
+  pass(r2, r0 * r0);
+}
+
 // ---- wave-owned variant -------------------------------------------------------------------
 // One wavefront transforms RW rows it owns.  A wave's LDS instructions are processed in order,
 // so the pass structure (all reads of a pass, then all writes) needs no s_barrier: the only
@@ -289,6 +326,16 @@ __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restr
   wave_pass<N, Pl::R0, 1, RW, PITCH, INV>(buf, tw, lane);
   if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV>(buf, tw, lane);
   if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw + Pl::T1, lane);
+}
+
+// length-N/2 transform of HalfPlan<N>; htw points at the appended tables (post twiddles first)
+template <int N, int PITCH, bool INV, typename T2>
+__device__ __forceinline__ void wave_fft_half(T2* __restrict__ buf, const T2* __restrict__ htw, int lane) {
+  using Hp = HalfPlan<N>;
+  static_assert(Hp::ok, "no half plan for this length");
+  wave_pass<Hp::H, Hp::R0, 1, 1, PITCH, INV>(buf, htw, lane);
+  wave_pass<Hp::H, Hp::R1, Hp::R0, 1, PITCH, INV>(buf, htw + Hp::P2, lane);
+  wave_pass<Hp::H, Hp::R2, Hp::R0 * Hp::R1, 1, PITCH, INV>(buf, htw + Hp::P3, lane);
 }
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for vmcnt(0), i.e. for

@@ -34,9 +34,13 @@ void Twiddles::build(int n_, bool fp64_) {
   n = n_;
   fp64 = fp64_;
   const double two_pi = 2.0 * std::acos(-1.0);
-  const int sz = fft_twiddle_size(n);
+  // N-point tables, then the z stage's real-signal half-transform tables (HalfPlan<n>)
+  const int sz0 = fft_twiddle_size(n);
+  const int sz = sz0 + fft_half_twiddle_size(n);
   std::vector<double2> h(sz, double2{1.0, 0.0});
-  fft_twiddle_fill(n, [&](int i, int m) { h[i] = double2{std::cos(two_pi * m / n), -std::sin(two_pi * m / n)}; });
+  auto w = [&](int m) { return double2{std::cos(two_pi * m / n), -std::sin(two_pi * m / n)}; };
+  fft_twiddle_fill(n, [&](int i, int m) { h[i] = w(m); });
+  fft_half_twiddle_fill(n, [&](int i, int m) { h[sz0 + i] = w(m); });
   if (fp64) {
     HIP_CHECK(hipMalloc(&buf, sz * sizeof(double2)));
     HIP_CHECK(hipMemcpy(buf, h.data(), sz * sizeof(double2), hipMemcpyHostToDevice));
@@ -423,7 +427,7 @@ constexpr int ZW = 4;
 template <int NZP, typename T>
 constexpr int zphys_rows() { return (sizeof(T) == 8 && NZP >= 2048) ? 2 : ZW; }
 
-template <int NZP, typename T, bool SEG, int ZWT = zphys_rows<NZP, T>()>
+template <int NZP, typename T, bool SEG, bool ZH = true, int ZWT = zphys_rows<NZP, T>()>
 __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -431,10 +435,14 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
   constexpr int EP = (NZP + 63) / 64;  // points per lane
   __shared__ T2 s[ZWT * PITCH];
   constexpr int TS = FftPlan<NZP>::TSIZE;
-  __shared__ T2 tws[TS];  // twiddles staged once per block: LDS latency instead of L2 in the passes
+  // real H_z: half-length complex transform + post twiddles (HalfPlan) where one exists
+  using Hp = HalfPlan<NZP>;
+  constexpr bool kHalf = ZH && Hp::ok;
+  constexpr int TSA = TS + (kHalf ? Hp::SIZE : 0);
+  __shared__ T2 tws[TSA];  // twiddles staged once per block: LDS latency instead of L2 in the passes
   __shared__ float red[4][ZWT];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < TS; i += ZWT * 64) tws[i] = tw[i];
+  for (int i = tid; i < TSA; i += ZWT * 64) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
@@ -563,6 +571,40 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       }
     }
     __builtin_amdgcn_wave_barrier();
+    if constexpr (kHalf) {
+      // H_z is real: z_m = Hz_2m + i Hz_2m+1 (scalar LDS stores, conflict-free), an N/2-point
+      // transform, then Hz_k = E_k + W_N^k O_k (one N-point complex transform per row saved)
+      T* rowf = reinterpret_cast<T*>(row);
+#pragma unroll
+      for (int i = 0; i < EP; ++i) {
+        const int n = lane + 64 * i;
+        if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+      const T2* htw = tws + TS;
+      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false>(row, htw, lane);
+      T2 z0[MKO], z1[MKO], wk[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx((Hp::H - k) & (Hp::H - 1))];
+          wk[i] = htw[k];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = lane + 64 * i;
+        if (k < nkz) {
+          // 2E = Z_k + conj Z_{H-k}; 2O = (Z_k - conj Z_{H-k}) / i
+          const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
+          const T2 O2{z0[i].y + z1[i].y, z1[i].x - z0[i].x};
+          const T2 X = cadd(E2, cmul_tw<false>(O2, wk[i]));
+          fields[2 * fs + zaddr(k)] = T2{X.x * sc, X.y * sc};
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < EP; ++i) {
       const int n = lane + 64 * i;
@@ -585,6 +627,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
         const int k = lane + 64 * i;
         if (k < nkz) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
       }
+    }
     }
   }
   // block maxima -> one atomicMax per block and quantity
@@ -876,19 +919,26 @@ static bool zreg_enabled() {
   return on;
 }
 
+// CHANNEL_ZHALF=0: H_z through a full-length complex transform (A/B of the half-length path)
+static bool zhalf_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_ZHALF");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <typename T>
 static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
+  const bool zh = zhalf_enabled();
   CH_DISPATCH_N(a.Nzp, {
     constexpr int ZR = zphys_rows<NN, T>();
     const long long nrows = static_cast<long long>(a.ny) * a.NX;
     dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
-    if (a.nseg > 1)
-      hipLaunchKernelGGL((zphys_kernel<NN, T, true>), grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields),
-                         static_cast<const T2*>(tw.buf));
-    else
-      hipLaunchKernelGGL((zphys_kernel<NN, T, false>), grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields),
-                         static_cast<const T2*>(tw.buf));
+    auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true> : zphys_kernel<NN, T, true, false>)
+                           : (zh ? zphys_kernel<NN, T, false, true> : zphys_kernel<NN, T, false, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
   });
   HIP_LAUNCH_CHECK(s);
 }
