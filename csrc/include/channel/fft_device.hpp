@@ -274,34 +274,54 @@ inline void fft_half_twiddle_fill(int n, F&& put) {  // put(index, m): entry hol
   pass(r2, r0 * r0);
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for vmcnt(0), i.e. for
+// every outstanding global load AND store of the wave (CDNA counts both on vmcnt), which
+// serialises a staging pipeline: each field's stores would have to be acknowledged by HBM before
+// the next field could be staged, and prefetched loads would be drained early.  Here only this
+// wave's LDS operations are waited for (lgkmcnt(0)) before s_barrier; the "memory" clobber keeps
+// the compiler from moving memory accesses across it.  Valid wherever the barrier only orders
+// LDS writes/reads between waves (global data exchanged between waves needs __syncthreads()).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Ordering of a row's LDS accesses between its threads: one wave (TPR = 64) only needs the
+// compiler to keep program order; a row shared by several waves needs the block barrier (every
+// thread of the block must then reach it).
+template <int TPR>
+__device__ __forceinline__ void row_sync() {
+  if constexpr (TPR == 64) __builtin_amdgcn_wave_barrier();
+  else lds_barrier();
+}
+
 // ---- wave-owned variant -------------------------------------------------------------------
 // One wavefront transforms RW rows it owns.  A wave's LDS instructions are processed in order,
 // so the pass structure (all reads of a pass, then all writes) needs no s_barrier: the only
 // requirement is that the compiler keeps the program order of the (possibly aliasing) LDS
 // accesses, which wave_barrier() pins.  Blocks then need barriers only around cooperative
 // global<->LDS staging, not per pass.
-template <int N, int R, int NS, int RW, int PITCH, bool INV, typename T2>
+// TPR threads (64: one wave; 128: two waves of one block) share the rows; lane = thread index
+// within them
+template <int N, int R, int NS, int RW, int PITCH, bool INV, int TPR = 64, typename T2>
 __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
   // tw: this pass's [R-1][NS] twiddle table
   constexpr int Q = N / R;
   constexpr int NB = RW * Q;
-  constexpr int B = (NB + 63) / 64;
+  constexpr int B = (NB + TPR - 1) / TPR;
   T2 v[B][R];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
-    const int idx = lane + b * 64;
-    if (NB % 64 == 0 || idx < NB) {
+    const int idx = lane + b * TPR;
+    if (NB % TPR == 0 || idx < NB) {
       const int row = idx / Q, j = idx - row * Q;
       const T2* p = buf + row * PITCH;
 #pragma unroll
       for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(j + r * Q)];
     }
   }
-  __builtin_amdgcn_wave_barrier();
+  row_sync<TPR>();
 #pragma unroll
   for (int b = 0; b < B; ++b) {
-    const int idx = lane + b * 64;
-    if (NB % 64 == 0 || idx < NB) {
+    const int idx = lane + b * TPR;
+    if (NB % TPR == 0 || idx < NB) {
       const int row = idx / Q, j = idx - row * Q;
       const int k = j & (NS - 1);
       if constexpr (NS > 1) {
@@ -317,35 +337,27 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       for (int r = 0; r < R; ++r) p[fft_pidx(base + r * NS)] = v[b][r];
     }
   }
-  __builtin_amdgcn_wave_barrier();
+  row_sync<TPR>();
 }
 
-template <int N, int RW, int PITCH, bool INV, typename T2>
+template <int N, int RW, int PITCH, bool INV, int TPR = 64, typename T2>
 __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
   using Pl = FftPlan<N>;
-  wave_pass<N, Pl::R0, 1, RW, PITCH, INV>(buf, tw, lane);
-  if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV>(buf, tw, lane);
-  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV>(buf, tw + Pl::T1, lane);
+  wave_pass<N, Pl::R0, 1, RW, PITCH, INV, TPR>(buf, tw, lane);
+  if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV, TPR>(buf, tw, lane);
+  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV, TPR>(buf, tw + Pl::T1, lane);
 }
 
 // length-N/2 transform of HalfPlan<N>; htw points at the appended tables (post twiddles first)
-template <int N, int PITCH, bool INV, typename T2>
+template <int N, int PITCH, bool INV, int TPR = 64, typename T2>
 __device__ __forceinline__ void wave_fft_half(T2* __restrict__ buf, const T2* __restrict__ htw, int lane) {
   using Hp = HalfPlan<N>;
   static_assert(Hp::ok, "no half plan for this length");
-  wave_pass<Hp::H, Hp::R0, 1, 1, PITCH, INV>(buf, htw, lane);
-  wave_pass<Hp::H, Hp::R1, Hp::R0, 1, PITCH, INV>(buf, htw + Hp::P2, lane);
-  wave_pass<Hp::H, Hp::R2, Hp::R0 * Hp::R1, 1, PITCH, INV>(buf, htw + Hp::P3, lane);
+  wave_pass<Hp::H, Hp::R0, 1, 1, PITCH, INV, TPR>(buf, htw, lane);
+  wave_pass<Hp::H, Hp::R1, Hp::R0, 1, PITCH, INV, TPR>(buf, htw + Hp::P2, lane);
+  wave_pass<Hp::H, Hp::R2, Hp::R0 * Hp::R1, 1, PITCH, INV, TPR>(buf, htw + Hp::P3, lane);
 }
 
-// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for vmcnt(0), i.e. for
-// every outstanding global load AND store of the wave (CDNA counts both on vmcnt), which
-// serialises a staging pipeline: each field's stores would have to be acknowledged by HBM before
-// the next field could be staged, and prefetched loads would be drained early.  Here only this
-// wave's LDS operations are waited for (lgkmcnt(0)) before s_barrier; the "memory" clobber keeps
-// the compiler from moving memory accesses across it.  Valid wherever the barrier only orders
-// LDS writes/reads between waves (global data exchanged between waves needs __syncthreads()).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so logical tiles that are adjacent in memory are given to blocks

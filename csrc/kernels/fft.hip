@@ -73,7 +73,13 @@ template <int NX, typename T, int WIDE = 0>
 struct XCfg {
   // kz columns per tile
   static constexpr int C = xcfg_c(NX, sizeof(T)) * (WIDE ? 2 : 1);
-  static constexpr int NT = xcfg_nt(WIDE, C);
+  // fp32 at 2048 points: the LDS holds one 8-column tile per CU, so that tile gets 8 waves, two per
+  // row (TPR = 128, block barriers between the passes; 2 waves per SIMD without spills) instead of
+  // 4 waves of 2 rows at one wave per SIMD
+  static constexpr bool BIG = NX >= 2048 && sizeof(T) == 4 && !WIDE;
+  static constexpr int NT = BIG ? 512 : xcfg_nt(WIDE, C);
+  static constexpr int MINB = BIG ? 1 : xcfg_minb(WIDE);
+  static constexpr int TPR = BIG ? 128 : 64;  // threads per transformed row
   // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
   // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
   static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
@@ -145,7 +151,7 @@ inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
 // SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
 // compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
 template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
-__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
@@ -208,11 +214,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
     {
-      constexpr int RW = C / (NT / 64);  // rows (kz columns) owned by each wave
+      constexpr int TPR = Cfg::TPR;
+      constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
       // one row at a time: the prefetched next tile already holds EPT registers
       if (!(a.diag & 1))
 #pragma unroll 1
-        for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, true>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+        for (int rr = 0; rr < RW; ++rr)
+          wave_fft<NX, 1, PITCH, true, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
@@ -233,7 +241,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
 }
 
 template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
-__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
@@ -281,11 +289,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), xcfg_minb(WIDE))
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
     {
-      constexpr int RW = C / (NT / 64);
+      constexpr int TPR = Cfg::TPR;
+      constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
       // one row at a time: the prefetched next tile already holds EPT registers
       if (!(a.diag & 1))
 #pragma unroll 1
-        for (int rr = 0; rr < RW; ++rr) wave_fft<NX, 1, PITCH, false>(s + ((tid / 64) * RW + rr) * PITCH, tws, tid & 63);
+        for (int rr = 0; rr < RW; ++rr)
+          wave_fft<NX, 1, PITCH, false, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
@@ -419,20 +429,27 @@ __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
   atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
 }
 
-// One wave per (y,x) row; a block holds ZWT rows and each wave owns one LDS row buffer, so there is
-// no block barrier between the gather, the five FFTs, the product and the extraction.  The six
-// physical fields stay in registers (each lane owns points n = lane + 64 i of the row).
+// One wave per (y,x) row up to 1024 points; a block holds ZWT rows and each wave owns one LDS row
+// buffer, so there is no block barrier between the gather, the five FFTs, the product and the
+// extraction.  The six physical fields stay in registers (thread t of a row owns points
+// n = t + TPR i).  2048-point rows take two waves (TPR = 128) with block barriers between the
+// passes: at one wave per row the 6 x 32 points per lane needed ~430 registers (one wave per
+// SIMD; 180 spilled VGPRs in fp64), at two waves the register budget of the 1024-point kernel.
 constexpr int ZW = 4;
-// rows per block: fp64 at 2048 points takes 2 (4 row buffers + twiddles would exceed the LDS)
+template <int NZP>
+constexpr int zphys_tpr() { return NZP >= 2048 ? 128 : 64; }
+// rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32)
 template <int NZP, typename T>
-constexpr int zphys_rows() { return (sizeof(T) == 8 && NZP >= 2048) ? 2 : ZW; }
+constexpr int zphys_rows() { return NZP >= 2048 ? 2 : ZW; }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int ZWT = zphys_rows<NZP, T>()>
-__global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+__global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>()) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int PITCH = FftPitch<NZP>::value;
-  constexpr int EP = (NZP + 63) / 64;  // points per lane
+  constexpr int TPR = zphys_tpr<NZP>();  // threads per row
+  constexpr int NWB = ZWT * TPR / 64;     // waves per block
+  constexpr int EP = (NZP + TPR - 1) / TPR;  // points per thread
   __shared__ T2 s[ZWT * PITCH];
   constexpr int TS = FftPlan<NZP>::TSIZE;
   // real H_z: half-length complex transform + post twiddles (HalfPlan) where one exists
@@ -440,9 +457,10 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
   constexpr bool kHalf = ZH && Hp::ok;
   constexpr int TSA = TS + (kHalf ? Hp::SIZE : 0);
   __shared__ T2 tws[TSA];  // twiddles staged once per block: LDS latency instead of L2 in the passes
-  __shared__ float red[4][ZWT];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < TSA; i += ZWT * 64) tws[i] = tw[i];
+  __shared__ float red[4][NWB];
+  // lane: wave lane (reductions); t: thread within the row; w: row within the block
+  const int tid = threadIdx.x, lane = tid & 63, t = tid % TPR, w = tid / TPR;
+  for (int i = tid; i < TSA; i += ZWT * TPR) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
@@ -460,15 +478,15 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
     }
   };
 
-  if (r < nrows) {  // wave-uniform
+  if (r < nrows) {  // block-uniform (nrows % ZWT == 0, checked on the host)
     T2 ph[3][EP];
-    constexpr int MK = (NZP / 2 + 63) / 64;
+    constexpr int MK = (NZP / 2 + TPR - 1) / TPR;
     auto fetch = [&](int p, T2 (&va)[MK], T2 (&vb)[MK]) {
       const T2* A = fields + (2 * p) * fs;
       const T2* B = fields + (2 * p + 1) * fs;
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         const long long o = k < nkz ? zaddr(k) : 0;
         va[i] = k < nkz ? A[o] : T2{0, 0};
         vb[i] = k < nkz ? B[o] : T2{0, 0};
@@ -493,7 +511,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
         const T2* B = fields + (2 * p + 1) * fs;
 #pragma unroll
         for (int i = 0; i < MK; ++i) {
-          const int k = lane + 64 * i;
+          const int k = t + TPR * i;
           const long long o = k < nkz ? zaddr(k) : 0;
           va[i] = k < nkz ? A[o] : T2{0, 0};
           vb[i] = k < nkz ? B[o] : T2{0, 0};
@@ -503,7 +521,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       // (a real z-row has a real mean), zero padding between Kz and N-Kz.
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           if (k == 0) {
             row[fft_pidx(0)] = T2{va[i].x, vb[i].x};
@@ -513,18 +531,18 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
           }
         }
       }
-      for (int k = Kz + 1 + lane; k < NZP - Kz; k += 64) row[fft_pidx(k)] = T2{0, 0};
+      for (int k = Kz + 1 + t; k < NZP - Kz; k += TPR) row[fft_pidx(k)] = T2{0, 0};
       if constexpr (kPrefetch) {
         if (p < 2) fetch(p + 1, pa, pb);
       }
-      __builtin_amdgcn_wave_barrier();
-      if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, true>(row, tws, lane);
+      row_sync<TPR>();
+      if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, true, TPR>(row, tws, t);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
-        const int n = lane + 64 * i;
+        const int n = t + TPR * i;
         ph[p][i] = n < NZP ? row[fft_pidx(n)] : T2{0, 0};
       }
-      __builtin_amdgcn_wave_barrier();
+      row_sync<TPR>();
     }
     // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
     const int yl = static_cast<int>(r / a.NX);
@@ -540,20 +558,20 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       mv = fmaxf(mv, av);
       mw = fmaxf(mw, aw);
       mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
-      const int n = lane + 64 * i;
+      const int n = t + TPR * i;
       if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
     }
-    __builtin_amdgcn_wave_barrier();
+    row_sync<TPR>();
     const T sc = static_cast<T>(0.5 * a.scale);
-    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
+    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false, TPR>(row, tws, t);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     // (unrolled: all LDS reads are issued before the global stores)
-    constexpr int MKO = (NZP / 2 + 63) / 64;
+    constexpr int MKO = (NZP / 2 + TPR - 1) / TPR;
     {
       T2 z0[MKO], z1[MKO];
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           z0[i] = row[fft_pidx(k)];
           z1[i] = row[fft_pidx((NZP - k) & (NZP - 1))];
@@ -561,7 +579,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       }
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           const T2 Z = z0[i], Zm = z1[i];
           const long long o = zaddr(k);
@@ -570,23 +588,23 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    row_sync<TPR>();
     if constexpr (kHalf) {
       // H_z is real: z_m = Hz_2m + i Hz_2m+1 (scalar LDS stores, conflict-free), an N/2-point
       // transform, then Hz_k = E_k + W_N^k O_k (one N-point complex transform per row saved)
       T* rowf = reinterpret_cast<T*>(row);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
-        const int n = lane + 64 * i;
+        const int n = t + TPR * i;
         if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
       }
-      __builtin_amdgcn_wave_barrier();
+      row_sync<TPR>();
       const T2* htw = tws + TS;
-      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false>(row, htw, lane);
+      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPR>(row, htw, t);
       T2 z0[MKO], z1[MKO], wk[MKO];
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           z0[i] = row[fft_pidx(k)];
           z1[i] = row[fft_pidx((Hp::H - k) & (Hp::H - 1))];
@@ -595,7 +613,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       }
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           // 2E = Z_k + conj Z_{H-k}; 2O = (Z_k - conj Z_{H-k}) / i
           const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
@@ -607,16 +625,16 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
     } else {
 #pragma unroll
     for (int i = 0; i < EP; ++i) {
-      const int n = lane + 64 * i;
+      const int n = t + TPR * i;
       if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
     }
-    __builtin_amdgcn_wave_barrier();
-    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false>(row, tws, lane);
+    row_sync<TPR>();
+    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false, TPR>(row, tws, t);
     {
       T2 z0[MKO], z1[MKO];
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) {
           z0[i] = row[fft_pidx(k)];
           z1[i] = row[fft_pidx((NZP - k) & (NZP - 1))];
@@ -624,7 +642,7 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
       }
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
-        const int k = lane + 64 * i;
+        const int k = t + TPR * i;
         if (k < nkz) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
       }
     }
@@ -638,15 +656,15 @@ __global__ void __launch_bounds__(64 * ZWT) zphys_kernel(ZArgs a, typename C2<T>
     mc = fmaxf(mc, __shfl_xor(mc, o));
   }
   if (lane == 0) {
-    red[0][w] = mu;
-    red[1][w] = mv;
-    red[2][w] = mw;
-    red[3][w] = mc;
+    red[0][tid >> 6] = mu;
+    red[1][tid >> 6] = mv;
+    red[2][tid >> 6] = mw;
+    red[3][tid >> 6] = mc;
   }
   __syncthreads();
   if (tid < 4 && a.maxima) {
     float m = 0.f;
-    for (int i = 0; i < ZWT; ++i) m = fmaxf(m, red[tid][i]);
+    for (int i = 0; i < NWB; ++i) m = fmaxf(m, red[tid][i]);
     atomic_max_pos(&a.maxima[tid], m);
   }
 }
@@ -938,7 +956,9 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
     dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
     auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true> : zphys_kernel<NN, T, true, false>)
                            : (zh ? zphys_kernel<NN, T, false, true> : zphys_kernel<NN, T, false, false>);
-    hipLaunchKernelGGL(kern, grid, dim3(64 * ZR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
+    CH_CHECK(nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
+    hipLaunchKernelGGL(kern, grid, dim3(ZR * zphys_tpr<NN>()), 0, s, a, static_cast<T2*>(fields),
+                       static_cast<const T2*>(tw.buf));
   });
   HIP_LAUNCH_CHECK(s);
 }
