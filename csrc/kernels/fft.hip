@@ -76,8 +76,9 @@ struct XCfg {
   // fp32 at 2048 points: the LDS holds one 8-column tile per CU, so that tile gets 8 waves, two per
   // row (TPR = 128, block barriers between the passes; 2 waves per SIMD without spills) instead of
   // 4 waves of 2 rows at one wave per SIMD
-  static constexpr bool BIG = NX >= 2048 && sizeof(T) == 4 && !WIDE;
-  static constexpr int NT = BIG ? 512 : xcfg_nt(WIDE, C);
+  // (fp64 from 1024 points likewise: 4 columns x 2 waves at 1024, 2 x 2 at 2048)
+  static constexpr bool BIG = NX >= (sizeof(T) == 4 ? 2048 : 1024) && !WIDE;
+  static constexpr int NT = BIG ? 128 * (C < 4 ? C : 4) : xcfg_nt(WIDE, C);
   static constexpr int MINB = BIG ? 1 : xcfg_minb(WIDE);
   static constexpr int TPR = BIG ? 128 : 64;  // threads per transformed row
   // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
@@ -437,17 +438,17 @@ __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
 // SIMD; 180 spilled VGPRs in fp64), at two waves the register budget of the 1024-point kernel.
 constexpr int ZW = 4;
 template <int NZP>
-constexpr int zphys_tpr() { return NZP >= 2048 ? 128 : 64; }
+constexpr int zphys_tpr(int esz = 4) { return NZP >= (esz == 4 ? 2048 : 1024) ? 128 : 64; }
 // rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32)
 template <int NZP, typename T>
 constexpr int zphys_rows() { return NZP >= 2048 ? 2 : ZW; }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int ZWT = zphys_rows<NZP, T>()>
-__global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>()) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+__global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int PITCH = FftPitch<NZP>::value;
-  constexpr int TPR = zphys_tpr<NZP>();  // threads per row
+  constexpr int TPR = zphys_tpr<NZP>(sizeof(T));  // threads per row
   constexpr int NWB = ZWT * TPR / 64;     // waves per block
   constexpr int EP = (NZP + TPR - 1) / TPR;  // points per thread
   __shared__ T2 s[ZWT * PITCH];
@@ -959,7 +960,7 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
                            : (zh ? zphys_kernel<NN, T, false, true> : zphys_kernel<NN, T, false, false>);
     dim3 grid(static_cast<unsigned>(nrows / ZR));
     CH_CHECK(nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
-    hipLaunchKernelGGL(kern, grid, dim3(ZR * zphys_tpr<NN>()), 0, s, a, static_cast<T2*>(fields),
+    hipLaunchKernelGGL(kern, grid, dim3(ZR * zphys_tpr<NN>(sizeof(T))), 0, s, a, static_cast<T2*>(fields),
                        static_cast<const T2*>(tw.buf));
   });
   HIP_LAUNCH_CHECK(s);
