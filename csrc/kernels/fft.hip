@@ -63,7 +63,7 @@ void Twiddles::release() {
 // fp64 at NX = 2048: 2 columns per tile (the 4-column tile plus the twiddles would exceed the
 // 160 KB of LDS), one wave per column
 constexpr int xcfg_c(int nx, int tsz) {
-  return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 2048 ? 2 : (nx >= 1024 ? 4 : 8));
+  return tsz == 4 ? (nx >= 1024 ? 8 : 16) : (nx >= 2048 ? 2 : (nx >= 1024 ? 4 : (nx >= 512 ? 8 : 16)));
 }
 // WIDE = 1: twice the kz columns per tile (128-B row segments) with 512 threads and one block per
 // CU (the same 8 waves per CU); WIDE = 0: 64-B segments, 256 threads, two blocks per CU.
@@ -217,11 +217,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
-      // one row at a time: the prefetched next tile already holds EPT registers
+      // one row at a time from 1024 points (the prefetched next tile already holds EPT registers);
+      // shorter rows RB at a time, so a radix-16 pass has 64 butterflies for the 64 lanes
+      constexpr int RB = (1024 / NX < 1 ? 1 : (1024 / NX < RW ? 1024 / NX : RW));  // 64 first-pass butterflies
       if (!(a.diag & 1))
 #pragma unroll 1
-        for (int rr = 0; rr < RW; ++rr)
-          wave_fft<NX, 1, PITCH, true, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+        for (int rr = 0; rr < RW; rr += RB)
+          wave_fft<NX, RB, PITCH, true, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
@@ -292,11 +294,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
-      // one row at a time: the prefetched next tile already holds EPT registers
+      // one row at a time from 1024 points (the prefetched next tile already holds EPT registers);
+      // shorter rows RB at a time, so a radix-16 pass has 64 butterflies for the 64 lanes
+      constexpr int RB = (1024 / NX < 1 ? 1 : (1024 / NX < RW ? 1024 / NX : RW));  // 64 first-pass butterflies
       if (!(a.diag & 1))
 #pragma unroll 1
-        for (int rr = 0; rr < RW; ++rr)
-          wave_fft<NX, 1, PITCH, false, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+        for (int rr = 0; rr < RW; rr += RB)
+          wave_fft<NX, RB, PITCH, false, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
@@ -436,12 +440,20 @@ __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
 // n = t + TPR i).  2048-point rows take two waves (TPR = 128) with block barriers between the
 // passes: at one wave per row the 6 x 32 points per lane needed ~430 registers (one wave per
 // SIMD; 180 spilled VGPRs in fp64), at two waves the register budget of the 1024-point kernel.
+// Below 1024 points a wave holds several rows (TPR < 64 threads per row): every thread keeps 16
+// (fp32) or 8 (fp64) points per field, and the wave's transforms cover all its rows at once, so a
+// 128-point row no longer leaves 56 of 64 lanes idle in its first radix-16 pass.
 constexpr int ZW = 4;
 template <int NZP>
-constexpr int zphys_tpr(int esz = 4) { return NZP >= (esz == 4 ? 2048 : 1024) ? 128 : 64; }
-// rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32)
+constexpr int zphys_tpr(int esz = 4) {
+  return esz == 4 ? (NZP >= 16 ? NZP / 16 : 1) : (NZP >= 1024 ? 128 : (NZP >= 16 ? NZP / 8 : 1));
+}
+// rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32);
+// 4 waves' worth of rows below 64 threads per row
 template <int NZP, typename T>
-constexpr int zphys_rows() { return NZP >= 2048 ? 2 : ZW; }
+constexpr int zphys_rows() {
+  return zphys_tpr<NZP>(sizeof(T)) < 64 ? ZW * 64 / zphys_tpr<NZP>(sizeof(T)) : (NZP >= 2048 ? 2 : ZW);
+}
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int ZWT = zphys_rows<NZP, T>()>
 __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
@@ -450,6 +462,8 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
   constexpr int PITCH = FftPitch<NZP>::value;
   constexpr int TPR = zphys_tpr<NZP>(sizeof(T));  // threads per row
   constexpr int NWB = ZWT * TPR / 64;     // waves per block
+  constexpr int TPRF = TPR < 64 ? 64 : TPR;  // threads per transform call (one wave or a row)
+  constexpr int RWW = TPR < 64 ? 64 / TPR : 1;  // rows per transform call
   constexpr int EP = (NZP + TPR - 1) / TPR;  // points per thread
   __shared__ T2 s[ZWT * PITCH];
   constexpr int TS = FftPlan<NZP>::TSIZE;
@@ -464,6 +478,8 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
   for (int i = tid; i < TSA; i += ZWT * TPR) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
+  T2* frow = s + (tid / TPRF) * RWW * PITCH;  // first row of this thread's transform group
+  const int ft = tid % TPRF;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   const long long r = static_cast<long long>(blockIdx.x) * ZWT + w;
   const int Kz = a.nkz - 1, nkz = a.nkz;
@@ -480,8 +496,10 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
   };
 
   // (a persistent variant looping over row groups made the compiler hold ~380 registers: one wave
-  // per SIMD, 49.8 vs 44.3 ms/step)
-  if (r < nrows) {  // block-uniform (nrows % ZWT == 0, checked on the host)
+  // per SIMD, 49.8 vs 44.3 ms/step).  Rows past the end (TPR < 64 only: the host checks
+  // nrows % ZWT == 0 otherwise) run the transforms on zeros and skip every global access.
+  const bool rv = r < nrows;
+  {
     T2 ph[3][EP];
     constexpr int MK = (NZP / 2 + TPR - 1) / TPR;
     auto fetch = [&](int p, T2 (&va)[MK], T2 (&vb)[MK]) {
@@ -490,9 +508,10 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
         const int k = t + TPR * i;
-        const long long o = k < nkz ? zaddr(k) : 0;
-        va[i] = k < nkz ? A[o] : T2{0, 0};
-        vb[i] = k < nkz ? B[o] : T2{0, 0};
+        const bool ld = k < nkz && rv;
+        const long long o = ld ? zaddr(k) : 0;
+        va[i] = ld ? A[o] : T2{0, 0};
+        vb[i] = ld ? B[o] : T2{0, 0};
       }
     };
     // the next pair's loads are in flight during each transform where the 24 registers fit (fp32,
@@ -515,9 +534,10 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
 #pragma unroll
         for (int i = 0; i < MK; ++i) {
           const int k = t + TPR * i;
-          const long long o = k < nkz ? zaddr(k) : 0;
-          va[i] = k < nkz ? A[o] : T2{0, 0};
-          vb[i] = k < nkz ? B[o] : T2{0, 0};
+          const bool ld = k < nkz && rv;
+          const long long o = ld ? zaddr(k) : 0;
+          va[i] = ld ? A[o] : T2{0, 0};
+          vb[i] = ld ? B[o] : T2{0, 0};
         }
       }
       // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
@@ -538,17 +558,17 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
       if constexpr (kPrefetch) {
         if (p < 2) fetch(p + 1, pa, pb);
       }
-      row_sync<TPR>();
-      if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, true, TPR>(row, tws, t);
+      row_sync<TPRF>();
+      if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, true, TPRF>(frow, tws, ft);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
         const int n = t + TPR * i;
         ph[p][i] = n < NZP ? row[fft_pidx(n)] : T2{0, 0};
       }
-      row_sync<TPR>();
+      row_sync<TPRF>();
     }
     // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
-    const int yl = static_cast<int>(r / a.NX);
+    const int yl = rv ? static_cast<int>(r / a.NX) : 0;
     const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
     T hz[EP];
 #pragma unroll
@@ -564,9 +584,9 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
       const int n = t + TPR * i;
       if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
     }
-    row_sync<TPR>();
+    row_sync<TPRF>();
     const T sc = static_cast<T>(0.5 * a.scale);
-    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false, TPR>(row, tws, t);
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     // (unrolled: all LDS reads are issued before the global stores)
     constexpr int MKO = (NZP / 2 + TPR - 1) / TPR;
@@ -583,7 +603,7 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
-        if (k < nkz) {
+        if (k < nkz && rv) {
           const T2 Z = z0[i], Zm = z1[i];
           const long long o = zaddr(k);
           fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
@@ -591,7 +611,7 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
         }
       }
     }
-    row_sync<TPR>();
+    row_sync<TPRF>();
     if constexpr (kHalf) {
       // H_z is real: z_m = Hz_2m + i Hz_2m+1 (scalar LDS stores, conflict-free), an N/2-point
       // transform, then Hz_k = E_k + W_N^k O_k (one N-point complex transform per row saved)
@@ -601,9 +621,9 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
         const int n = t + TPR * i;
         if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
       }
-      row_sync<TPR>();
+      row_sync<TPRF>();
       const T2* htw = tws + TS;
-      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPR>(row, htw, t);
+      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPRF>(row, htw, ft);
       T2 z0[MKO], z1[MKO], wk[MKO];
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
@@ -617,7 +637,7 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
-        if (k < nkz) {
+        if (k < nkz && rv) {
           // 2E = Z_k + conj Z_{H-k}; 2O = (Z_k - conj Z_{H-k}) / i
           const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
           const T2 O2{z0[i].y + z1[i].y, z1[i].x - z0[i].x};
@@ -631,8 +651,8 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
       const int n = t + TPR * i;
       if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
     }
-    row_sync<TPR>();
-    if (!(a.diag & 1)) wave_fft<NZP, 1, PITCH, false, TPR>(row, tws, t);
+    row_sync<TPRF>();
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
     {
       T2 z0[MKO], z1[MKO];
 #pragma unroll
@@ -646,7 +666,7 @@ __global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
-        if (k < nkz) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
+        if (k < nkz && rv) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
       }
     }
     }
@@ -958,8 +978,8 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
     const long long nrows = static_cast<long long>(a.ny) * a.NX;
     auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true> : zphys_kernel<NN, T, true, false>)
                            : (zh ? zphys_kernel<NN, T, false, true> : zphys_kernel<NN, T, false, false>);
-    dim3 grid(static_cast<unsigned>(nrows / ZR));
-    CH_CHECK(nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
+    dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
+    CH_CHECK(zphys_tpr<NN>(sizeof(T)) < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
     hipLaunchKernelGGL(kern, grid, dim3(ZR * zphys_tpr<NN>(sizeof(T))), 0, s, a, static_cast<T2*>(fields),
                        static_cast<const T2*>(tw.buf));
   });
