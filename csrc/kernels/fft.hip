@@ -450,17 +450,18 @@ constexpr int zphys_tpr(int esz = 4) {
 }
 // rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32);
 // 4 waves' worth of rows below 64 threads per row
-template <int NZP, typename T>
+template <int NZP, typename T, int TPR = zphys_tpr<NZP>(sizeof(T))>
 constexpr int zphys_rows() {
-  return zphys_tpr<NZP>(sizeof(T)) < 64 ? ZW * 64 / zphys_tpr<NZP>(sizeof(T)) : (NZP >= 2048 ? 2 : ZW);
+  return TPR < 64 ? ZW * 64 / TPR : (NZP >= 2048 || (sizeof(T) == 4 && TPR == 128) ? 2 : ZW);
 }
 
-template <int NZP, typename T, bool SEG, bool ZH = true, int ZWT = zphys_rows<NZP, T>()>
-__global__ void __launch_bounds__(ZWT * zphys_tpr<NZP>(sizeof(T))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
+          int ZWT = zphys_rows<NZP, T, TPRT>()>
+__global__ void __launch_bounds__(ZWT * TPRT) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int PITCH = FftPitch<NZP>::value;
-  constexpr int TPR = zphys_tpr<NZP>(sizeof(T));  // threads per row
+  constexpr int TPR = TPRT;  // threads per row
   constexpr int NWB = ZWT * TPR / 64;     // waves per block
   constexpr int TPRF = TPR < 64 ? 64 : TPR;  // threads per transform call (one wave or a row)
   constexpr int RWW = TPR < 64 ? 64 / TPR : 1;  // rows per transform call
@@ -969,19 +970,41 @@ static bool zhalf_enabled() {
   return on;
 }
 
+template <int NN, typename T, int TPR>
+static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s, bool zh) {
+  using T2 = typename C2<T>::type;
+  constexpr int ZR = zphys_rows<NN, T, TPR>();
+  const long long nrows = static_cast<long long>(a.ny) * a.NX;
+  auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR> : zphys_kernel<NN, T, true, false, TPR>)
+                         : (zh ? zphys_kernel<NN, T, false, true, TPR> : zphys_kernel<NN, T, false, false, TPR>);
+  dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
+  CH_CHECK(TPR < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
+  hipLaunchKernelGGL(kern, grid, dim3(ZR * TPR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
+}
+
+// CHANNEL_ZTPR=64|128: threads per 1024-point fp32 row (A/B; see zphys_tpr for the default).  Two
+// waves per row take 152 instead of 218 VGPRs (3 waves/SIMD) but pay a block barrier per pass:
+// measured 48.8 vs 46.3 ms/step on the headline grid, so one wave per row stays the default.
+static int ztpr_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_ZTPR");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <typename T>
 static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s) {
-  using T2 = typename C2<T>::type;
   const bool zh = zhalf_enabled();
   CH_DISPATCH_N(a.Nzp, {
-    constexpr int ZR = zphys_rows<NN, T>();
-    const long long nrows = static_cast<long long>(a.ny) * a.NX;
-    auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true> : zphys_kernel<NN, T, true, false>)
-                           : (zh ? zphys_kernel<NN, T, false, true> : zphys_kernel<NN, T, false, false>);
-    dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
-    CH_CHECK(zphys_tpr<NN>(sizeof(T)) < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
-    hipLaunchKernelGGL(kern, grid, dim3(ZR * zphys_tpr<NN>(sizeof(T))), 0, s, a, static_cast<T2*>(fields),
-                       static_cast<const T2*>(tw.buf));
+    constexpr int DEF = zphys_tpr<NN>(sizeof(T));
+    if constexpr (sizeof(T) == 4 && NN == 1024) {
+      constexpr int ALT = DEF == 64 ? 128 : 64;
+      if (ztpr_env() == ALT) zphys_launch_tpr<NN, T, ALT>(a, fields, tw, s, zh);
+      else zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
+    } else {
+      zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
+    }
   });
   HIP_LAUNCH_CHECK(s);
 }
