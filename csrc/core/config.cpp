@@ -263,7 +263,7 @@ void Config::validate() const {
   CH_CHECK(is_pow2(NX) && NX >= 16 && NX <= 4096, "NX=" << NX << " must be a power of two in [16, 4096]");
   CH_CHECK(NZ >= 9 && is_pow2(2 * NZ - 2) && 2 * NZ - 2 <= 4096,
            "2*NZ-2=" << (2 * NZ - 2) << " (physical z points) must be a power of two in [16, 4096]");
-  CH_CHECK(NY >= 9 && NY <= 64 * 16, "NY=" << NY << " must be in [9, 1024]");
+  CH_CHECK(NY >= 9 && NY <= 64 * 24, "NY=" << NY << " must be in [9, 1536]");
   CH_CHECK(Re > 0 && Q > 0 && LX > 0 && LZ > 0, "Re, Q, LX, LZ must be positive");
   CH_CHECK(stretch > 0, "stretch must be positive");
   CH_CHECK(cfl > 0, "cfl must be positive");

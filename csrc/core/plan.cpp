@@ -85,7 +85,7 @@ Plan Plan::make(const Config& cfg, int P, int rank) {
   p.nx_loc = p.x_split.count[p.prow];
   p.x0 = p.x_split.start[p.prow];
   p.R = (p.NY + 63) / 64;
-  CH_CHECK(p.R <= 16, "NY too large for the y-line solver (max 1024)");
+  CH_CHECK(p.R <= 24, "NY too large for the y-line solver (max 1536)");
   const double two_pi = 2.0 * std::acos(-1.0);
   p.ax = two_pi / cfg.LX;
   p.az = two_pi / cfg.LZ;

@@ -40,10 +40,10 @@ struct Cplx<double> {
 };
 
 int yline_supported_R(int NY) {
-  static const int supported[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16};
+  static const int supported[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16, 24};
   for (int r : supported)
     if (64 * r >= NY) return r;
-  CH_CHECK(false, "NY=" << NY << " too large for the y-line kernels (max 1024)");
+  CH_CHECK(false, "NY=" << NY << " too large for the y-line kernels (max 1536)");
 }
 
 #define CH_DISPATCH_R(R_, ...)                       \
@@ -59,6 +59,7 @@ int yline_supported_R(int NY) {
     case 10: { constexpr int R = 10; __VA_ARGS__; } break;  \
     case 12: { constexpr int R = 12; __VA_ARGS__; } break;  \
     case 16: { constexpr int R = 16; __VA_ARGS__; } break;  \
+    case 24: { constexpr int R = 24; __VA_ARGS__; } break;  \
     default: CH_CHECK(false, "unsupported R=" << R_); \
   }
 

@@ -15,7 +15,7 @@ def rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
 
 
-@pytest.mark.parametrize("NY", [33, 65, 129, 257, 385, 633])
+@pytest.mark.parametrize("NY", [33, 65, 129, 257, 385, 633, 1100])
 @pytest.mark.parametrize("dtype", [torch.complex128, torch.complex64])
 def test_yline_operators(native, NY, dtype):
     rng = np.random.default_rng(NY)

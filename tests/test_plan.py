@@ -115,3 +115,12 @@ def test_bench_refuses_work_skipping_env(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "1"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "work-skipping" in (r.stderr + r.stdout)
+
+
+def test_ny_cap_lifted_to_1536(native):
+    """The reference's one-thread-per-y-point solver caps NY at 1024 (main.c:79-82); the register-
+    resident y-line kernels go to R = 24 rows per lane (NY <= 1536), beyond which Plan refuses."""
+    assert native.Plan.make(cfg(native, NX=32, NY=1201, NZ=17), 1, 0).R == 19
+    assert native.Plan.make(cfg(native, NX=32, NY=1536, NZ=17), 1, 0).R == 24
+    with pytest.raises(Exception, match="1536"):
+        native.Plan.make(cfg(native, NX=32, NY=1537, NZ=17), 1, 0)

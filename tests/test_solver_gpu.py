@@ -42,10 +42,12 @@ def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
 
 
 @pytest.mark.parametrize("precision,NY", [("fp32", 129), ("fp64", 129), ("fp32", 257), ("fp64", 257), ("fp32", 385),
-                                          ("fp32", 633), ("fp64", 633), ("fp32", 769)])
+                                          ("fp32", 633), ("fp64", 633), ("fp32", 769), ("fp32", 1201),
+                                          ("fp64", 1409)])
 def test_gpu_matches_oracle_large_ny(native, precision, NY):
     """Tall lines: R = 3, 4 (address-only prefetch slots), R = 7 (register prefetch slots),
-    R = 10 and 13->16 (deferred slots, LDS-staged tables)."""
+    R = 10 and 13->16 (deferred slots, LDS-staged tables), 17->24 (NY up to 1536: the lifted
+    NY <= 1024 cap of the reference, main.c:79-82)."""
     NX, NZ, dt = 16, 9, 1e-4
     kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision=precision, dt_fixed=dt, stats_every=0, log_every=0,
               symmetry_every=0, ic="zero")
@@ -55,7 +57,8 @@ def test_gpu_matches_oracle_large_ny(native, precision, NY):
     if precision == "fp32":
         phi = phi.astype(np.complex64).astype(np.complex128)
         om = om.astype(np.complex64).astype(np.complex128)
-    tol, tolU = (1e-9, 1e-11) if precision == "fp64" else (1e-4, 1e-5)  # fp32 storage round-off grows with NY
+    # fp32 storage round-off grows with NY (omega at NY = 1201: 1.2e-4)
+    tol, tolU = (1e-9, 1e-11) if precision == "fp64" else (1e-4 * max(1.0, NY / 600), 1e-5)
     U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
     o.set_state(phi, om, U)
     s.set_state(phi, om, U)
