@@ -456,8 +456,8 @@ constexpr int zphys_rows() {
 }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
-          int ZWT = zphys_rows<NZP, T, TPRT>()>
-__global__ void __launch_bounds__(ZWT * TPRT) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 1>
+__global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   constexpr int PITCH = FftPitch<NZP>::value;
@@ -970,13 +970,13 @@ static bool zhalf_enabled() {
   return on;
 }
 
-template <int NN, typename T, int TPR>
+template <int NN, typename T, int TPR, int WPE = 1>
 static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s, bool zh) {
   using T2 = typename C2<T>::type;
   constexpr int ZR = zphys_rows<NN, T, TPR>();
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
-  auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR> : zphys_kernel<NN, T, true, false, TPR>)
-                         : (zh ? zphys_kernel<NN, T, false, true, TPR> : zphys_kernel<NN, T, false, false, TPR>);
+  auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
+                         : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
   dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
   CH_CHECK(TPR < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
   hipLaunchKernelGGL(kern, grid, dim3(ZR * TPR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
@@ -985,6 +985,15 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
 // CHANNEL_ZTPR=64|128: threads per 1024-point fp32 row (A/B; see zphys_tpr for the default).  Two
 // waves per row take 152 instead of 218 VGPRs (3 waves/SIMD) but pay a block barrier per pass:
 // measured 48.8 vs 46.3 ms/step on the headline grid, so one wave per row stays the default.
+// CHANNEL_ZWPE=3: the one-wave-per-row 1024-point fp32 kernel compiled for 3 waves per SIMD (168
+// VGPRs, ~20 spilled) instead of 2 (216 VGPRs, no spills) (A/B)
+static int zwpe_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_ZWPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 static int ztpr_env() {
   static const int v = [] {
     const char* e = std::getenv("CHANNEL_ZTPR");
@@ -1001,6 +1010,7 @@ static void zphys_launch(const ZArgs& a, void* fields, const Twiddles& tw, hipSt
     if constexpr (sizeof(T) == 4 && NN == 1024) {
       constexpr int ALT = DEF == 64 ? 128 : 64;
       if (ztpr_env() == ALT) zphys_launch_tpr<NN, T, ALT>(a, fields, tw, s, zh);
+      else if (DEF == 64 && zwpe_env() == 3) zphys_launch_tpr<NN, T, DEF, 3>(a, fields, tw, s, zh);
       else zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
     } else {
       zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
