@@ -986,7 +986,8 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
 // waves per row take 152 instead of 218 VGPRs (3 waves/SIMD) but pay a block barrier per pass:
 // measured 48.8 vs 46.3 ms/step on the headline grid, so one wave per row stays the default.
 // CHANNEL_ZWPE=3: the one-wave-per-row 1024-point fp32 kernel compiled for 3 waves per SIMD (168
-// VGPRs, ~20 spilled) instead of 2 (216 VGPRs, no spills) (A/B)
+// VGPRs, ~20 spilled) instead of 2 (216 VGPRs, no spills) (A/B).  Measured on the headline grid,
+// same box, alternating: 47.4 vs 45.5 ms/step, so 2 waves per SIMD without spills stays the default
 static int zwpe_env() {
   static const int v = [] {
     const char* e = std::getenv("CHANNEL_ZWPE");
