@@ -38,7 +38,8 @@ def reference_preset(name: str, **kw):
         "poiseuille": dict(NX=32, NY=33, NZ=17, Re=100.0, ic="laminar", precision="fp64"),
         # reference run.conf grid (128 x 128 x 128 physical, Re=3250)
         "ref128": dict(NX=128, NY=129, NZ=65, Re=3250.0, precision="fp32"),
-        "retau180": dict(NX=128, NY=129, NZ=65, Re=3250.0, precision="fp64"),
+        # Re = 3130 gives Re_tau ~ 180 at Q = 1.8 (configs/retau180_128x129x128.conf, the validation run)
+        "retau180": dict(NX=128, NY=129, NZ=65, Re=3130.0, precision="fp64"),
         "retau550": dict(NX=512, NY=257, NZ=257, Re=11150.0, precision="fp32"),
         "retau950": dict(NX=1024, NY=385, NZ=513, Re=20700.0, precision="fp32"),
         "retau2000": dict(NX=2048, NY=633, NZ=1025, Re=48300.0, precision="fp32"),

@@ -75,19 +75,27 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
     sockaddr_in sa{};
     sa.sin_family = AF_INET;
     sa.sin_port = htons(static_cast<uint16_t>(port));
-    // listen on MASTER_ADDR (the address the peers connect to), not on every interface
+    // Listen on every interface: a MASTER_ADDR hostname may resolve to a loopback alias on the
+    // master (127.0.1.1 via /etc/hosts) or to an address that is not local (NAT), and binding to it
+    // would strand the remote peers.  The peers are checked by their announced rank below.
+    // CHANNEL_BOOTSTRAP_BIND_MASTER=1 binds to MASTER_ADDR instead (falling back to every interface
+    // when it resolves to loopback or the bind fails).
     sa.sin_addr.s_addr = htonl(INADDR_ANY);
-    {
+    bool bound = false;
+    if (const char* bm = std::getenv("CHANNEL_BOOTSTRAP_BIND_MASTER"); bm && std::atoi(bm) == 1) {
       addrinfo hints{}, *res = nullptr;
       hints.ai_family = AF_INET;
       hints.ai_socktype = SOCK_STREAM;
       if (getaddrinfo(addr.c_str(), nullptr, &hints, &res) == 0 && res) {
-        sa.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
+        sockaddr_in m = sa;
+        m.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
         freeaddrinfo(res);
+        const bool loop = (ntohl(m.sin_addr.s_addr) >> 24) == 127;
+        bound = !loop && ::bind(ls, reinterpret_cast<sockaddr*>(&m), sizeof(m)) == 0;
       }
     }
-    CH_CHECK(::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0,
-             "bind to " << addr << ":" << port << " failed");
+    CH_CHECK(bound || ::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0,
+             "bootstrap: bind to port " << port << " failed");
     CH_CHECK(::listen(ls, pi.size) == 0, "listen failed");
     std::vector<bool> seen(pi.size, false);
     seen[0] = true;

@@ -257,12 +257,20 @@ std::vector<int> Config::spectra_plane_list() const {
   return out;
 }
 
-static bool is_pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+// transform lengths with kernels (kernels/fft.hip CH_DISPATCH_N): 2^k in [16, 2048], 3*2^k in
+// [48, 1536], 5*2^k in [80, 1280] (the reference's cuFFT plans take any length, fft.c:17-23)
+bool fft_length_supported(int n) {
+  if (n < 16 || n > 2048) return false;
+  int m = n;
+  if (m % 3 == 0) m /= 3;
+  else if (m % 5 == 0) m /= 5;
+  return (m & (m - 1)) == 0 && m >= 16;
+}
 
 void Config::validate() const {
-  CH_CHECK(is_pow2(NX) && NX >= 16 && NX <= 4096, "NX=" << NX << " must be a power of two in [16, 4096]");
-  CH_CHECK(NZ >= 9 && is_pow2(2 * NZ - 2) && 2 * NZ - 2 <= 4096,
-           "2*NZ-2=" << (2 * NZ - 2) << " (physical z points) must be a power of two in [16, 4096]");
+  CH_CHECK(fft_length_supported(NX), "NX=" << NX << " must be 2^k (16..2048), 3*2^k (48..1536) or 5*2^k (80..1280)");
+  CH_CHECK(NZ >= 9 && fft_length_supported(2 * NZ - 2),
+           "2*NZ-2=" << (2 * NZ - 2) << " (physical z points) must be 2^k (16..2048), 3*2^k (48..1536) or 5*2^k (80..1280)");
   CH_CHECK(NY >= 9 && NY <= 64 * 24, "NY=" << NY << " must be in [9, 1536]");
   CH_CHECK(Re > 0 && Q > 0 && LX > 0 && LZ > 0, "Re, Q, LX, LZ must be positive");
   CH_CHECK(stretch > 0, "stretch must be positive");

@@ -118,6 +118,9 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
   if (nranks > 1 || !nccl_uid.empty()) {
     CH_CHECK(!nccl_uid.empty(), "P > 1 requires an RCCL unique id");
     comm_ = Comm::create(rank, nranks, nccl_uid, device_);
+    // per-run nonce shared by all ranks without a collective: FNV-1a of the communicator id
+    run_nonce_ = 1469598103934665603ULL;
+    for (unsigned char ch : nccl_uid) run_nonce_ = (run_nonce_ ^ ch) * 1099511628211ULL;
     // RCCL exchanges are captured into the step graph like everything else (the first step runs
     // eagerly so RCCL sets up its peer connections outside capture); CHANNEL_GRAPH_MULTI=0 keeps
     // multi-rank steps eager.  The host-staged ShmComm is never capturable.
@@ -975,6 +978,26 @@ void Solver::step(bool stats_for_next) {
         use_graph_ = false;
       }
       graph_ok_[gi] = true;
+      if (comm_ && plan_.P > 1) {
+        // every rank must replay the same exchange sequence: if capture failed anywhere, all ranks
+        // drop their graphs and step eagerly (no rank may launch a captured RCCL sequence that a
+        // peer runs eagerly in a different order)
+        unsigned* flag = d_health_ + 1;
+        const unsigned mine = gexec_[gi] ? 0u : 1u;
+        HIP_CHECK(hipMemcpyAsync(flag, &mine, sizeof(unsigned), hipMemcpyHostToDevice, s_comm_));
+        comm_->allreduce_max_u32(flag, 1, s_comm_);
+        unsigned any = 0;
+        HIP_CHECK(hipMemcpyAsync(&any, flag, sizeof(unsigned), hipMemcpyDeviceToHost, s_comm_));
+        wait(s_comm_);
+        if (any) {
+          if (gexec_[gi]) {
+            (void)hipGraphExecDestroy(gexec_[gi]);
+            gexec_[gi] = nullptr;
+            std::cerr << "[channel] hipGraph capture failed on a peer rank: every rank runs eagerly\n";
+          }
+          use_graph_ = false;
+        }
+      }
     }
     if (gexec_[gi]) {
       HIP_CHECK(hipGraphLaunch(gexec_[gi], s_comp_));
@@ -1547,11 +1570,16 @@ void Solver::checkpoint_async(const std::string& g, const std::string& ddv, cons
   ckpt_thread_ = std::thread([this, j = std::move(j), P, rank, timeout]() {
     try {
       // turn t belongs to rank t % P: rank r waits for the marker "<g>.turn" holding
-      // "<serial> <t>" written by the previous writer (atomic rename), then passes it on
+      // "<run nonce> <serial> <t>" written by the previous writer (atomic rename), then passes it
+      // on.  The nonce (from the communicator id) keeps a marker left behind by a crashed earlier
+      // run of the same path from ever matching; rank 0 also removes any marker before its first
+      // turn (it writes first, so nobody can be waiting on a current one yet).
       const std::string marker = (j.g != "-" ? j.g : j.ddv) + ".turn";
+      const std::string tag = std::to_string(run_nonce_) + " " + std::to_string(j.serial) + " ";
+      if (P > 1 && rank == 0) std::remove(marker.c_str());
       auto wait_turn = [&](int t) {
         if (P == 1 || t == 0) return;
-        const std::string want = std::to_string(j.serial) + " " + std::to_string(t);
+        const std::string want = tag + std::to_string(t);
         const auto t0 = std::chrono::steady_clock::now();
         while (true) {
           std::ifstream f(marker);
@@ -1567,7 +1595,7 @@ void Solver::checkpoint_async(const std::string& g, const std::string& ddv, cons
         const std::string tmp = marker + "." + std::to_string(rank);
         {
           std::ofstream f(tmp, std::ios::trunc);
-          f << j.serial << " " << t << "\n";
+          f << tag << t << "\n";
         }
         CH_CHECK(std::rename(tmp.c_str(), marker.c_str()) == 0, "checkpoint: cannot update " << marker);
       };
@@ -1619,12 +1647,25 @@ void Solver::read_restart(const std::string& g, const std::string& ddv, const st
   unpack(ddv, phi);
   std::vector<double> U(N, 0.0);
   std::vector<double> u64;
-  if (h5_read_vector(g, "umean", u64) && static_cast<int>(u64.size()) == N) {
-    // written by this framework: U at full precision (preferred over the float32 UMEAN file)
-    for (int jy = 0; jy < N; ++jy) U[jy] = u64[jy] / N2;
-  } else if (!umean.empty() && umean != "-") {
+  const bool umean_given = !umean.empty() && umean != "-";
+  if (umean_given) {
+    // an explicitly named UMEAN file wins (the reference's float32 records, meanUevol.c:153-176);
+    // when it is the companion of G (the same profile rounded to float32), the full-precision copy
+    // inside G is used instead
     U = umean_read(umean, N);
+    bool companion = h5_read_vector(g, "umean", u64) && static_cast<int>(u64.size()) == N;
+    for (int jy = 0; companion && jy < N; ++jy)
+      companion = static_cast<float>(u64[jy]) == static_cast<float>(U[jy]);
+    if (companion) {
+      U = u64;
+    } else if (plan_.rank == 0 && !u64.empty()) {
+      std::cerr << "[channel] read_restart: U(y) from " << umean << " (differs from the 'umean' stored in " << g
+                << ", which is ignored)\n";
+    }
     for (auto& u : U) u /= N2;
+  } else if (h5_read_vector(g, "umean", u64) && static_cast<int>(u64.size()) == N) {
+    // no UMEAN file named: U at full precision from the G file written by this framework
+    for (int jy = 0; jy < N; ++jy) U[jy] = u64[jy] / N2;
   } else {
     const auto& y = grid_.y;
     for (int j = 0; j < N; ++j) U[j] = 0.75 * cfg_.Q * (1.0 - y[j] * y[j]);

@@ -96,4 +96,7 @@ struct Config {
   std::vector<int> spectra_plane_list() const;   // parsed spectra_planes (default {NY/2})
 };
 
+// FFT lengths the transform kernels are instantiated for: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280)
+bool fft_length_supported(int n);
+
 }  // namespace channel

@@ -1,15 +1,18 @@
-// In-LDS batched complex FFT (Stockham autosort, mixed radix 16/8/4/2, radix-16 first).
+// In-LDS batched complex FFT (Stockham autosort, mixed radix 16/12/10/8/6/5/4/3/2, radix 16 first).
 //
 // All threads of the workgroup cooperate on ROWS rows of length N held in LDS.  Each pass gathers
 // its butterfly inputs into registers, synchronises, applies the inter-pass twiddles and an R-point
 // DFT in registers, and writes the outputs back in place.  LDS addresses are padded by one slot per
 // 16 elements (fft_pidx): with radix-16 first passes every store lane-stride becomes 17 elements
 // (34 dwords), which is conflict-free for ds_write_b64, and the strided reads stay contiguous.
-// Radix plans: 16, 16x2, 16x4, 16x8, 16x16, 16x16x2, 16x16x4, 16x16x8 (N = 16 ... 2048): at most
-// three LDS round trips per transform (the radix-4-only version needed log4 N + 1).
+// Radix plans (fft_radices): powers of two 16, 16x2, ..., 16x16x8 (N = 16 ... 2048), and the
+// lengths 3*2^k and 5*2^k from 48 / 80 with the odd factor in the last pass (e.g. 96 = 16x6,
+// 384 = 16x8x3, 768 = 16x16x3, 1536 = 16x16x6, 1280 = 16x16x5): at most three LDS round trips per
+// transform (the radix-4-only version needed log4 N + 1).
 // Twiddles come from per-pass tables (FftPlan::T1/T2, built by fft_twiddle_fill), staged in LDS.
 //
-// Replaces the reference's cuFFT 2-D plans (fft.c:17-23); length is a compile-time power of two.
+// Replaces the reference's cuFFT 2-D plans (fft.c:17-23), which take any NX and 2NZ-2; the length
+// is a compile-time constant of the form 2^a 3^b 5^c with b + c <= 1.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -97,7 +100,6 @@ __device__ __forceinline__ T2 mul_mi(T2 d) {
   }
 }
 
-constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
 
 // padded LDS index of logical element p of a row
 __device__ __forceinline__ constexpr int fft_pidx(int p) { return p + (p >> 4); }
@@ -188,23 +190,142 @@ __device__ __forceinline__ void dft16(T2* v) {
   }
 }
 
+// odd radices (forward sign e^{-2 pi i nk/R}; INV flips it)
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft3(T2* v) {
+  using T = decltype(v[0].x);
+  const T s = static_cast<T>(0.86602540378443864676);  // sin 60
+  const T2 t1 = cadd(v[1], v[2]), d = csub(v[1], v[2]);
+  const T2 t2{v[0].x - T(0.5) * t1.x, v[0].y - T(0.5) * t1.y};
+  const T2 m = mul_mi<INV>(T2{s * d.x, s * d.y});  // -i s d (forward)
+  v[0] = cadd(v[0], t1);
+  v[1] = cadd(t2, m);
+  v[2] = csub(t2, m);
+}
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft5(T2* v) {
+  using T = decltype(v[0].x);
+  const T c1 = static_cast<T>(0.30901699437494742410), c2 = static_cast<T>(-0.80901699437494742410);
+  const T s1 = static_cast<T>(0.95105651629515357212), s2 = static_cast<T>(0.58778525229247312917);
+  const T2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]), t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+  const T2 a1{v[0].x + c1 * t1.x + c2 * t2.x, v[0].y + c1 * t1.y + c2 * t2.y};
+  const T2 a2{v[0].x + c2 * t1.x + c1 * t2.x, v[0].y + c2 * t1.y + c1 * t2.y};
+  const T2 b1 = mul_mi<INV>(T2{s1 * t3.x + s2 * t4.x, s1 * t3.y + s2 * t4.y});  // -i b1 (forward)
+  const T2 b2 = mul_mi<INV>(T2{s2 * t3.x - s1 * t4.x, s2 * t3.y - s1 * t4.y});
+  v[0] = cadd(v[0], cadd(t1, t2));
+  v[1] = cadd(a1, b1);
+  v[4] = csub(a1, b1);
+  v[2] = cadd(a2, b2);
+  v[3] = csub(a2, b2);
+}
+
+// W_R^m = exp(-2 pi i m / R) (forward sign) for the composite radices, compile-time tables
+template <int R>
+struct RootTable;
+template <>
+struct RootTable<6> {
+  static constexpr double c[6] = {1.0, 0.5, -0.5, -1.0, -0.5, 0.5};
+  static constexpr double s[6] = {0.0, 0.86602540378443864676, 0.86602540378443864676, 0.0,
+                                  -0.86602540378443864676, -0.86602540378443864676};
+};
+template <>
+struct RootTable<10> {
+  static constexpr double c[10] = {1.0, 0.80901699437494742410, 0.30901699437494742410, -0.30901699437494742410,
+                                   -0.80901699437494742410, -1.0, -0.80901699437494742410, -0.30901699437494742410,
+                                   0.30901699437494742410, 0.80901699437494742410};
+  static constexpr double s[10] = {0.0, 0.58778525229247312917, 0.95105651629515357212, 0.95105651629515357212,
+                                   0.58778525229247312917, 0.0, -0.58778525229247312917, -0.95105651629515357212,
+                                   -0.95105651629515357212, -0.58778525229247312917};
+};
+template <>
+struct RootTable<12> {
+  static constexpr double c[12] = {1.0, 0.86602540378443864676, 0.5, 0.0, -0.5, -0.86602540378443864676,
+                                   -1.0, -0.86602540378443864676, -0.5, 0.0, 0.5, 0.86602540378443864676};
+  static constexpr double s[12] = {0.0, 0.5, 0.86602540378443864676, 1.0, 0.86602540378443864676, 0.5,
+                                   0.0, -0.5, -0.86602540378443864676, -1.0, -0.86602540378443864676, -0.5};
+};
+
+template <int R, bool INV, typename T2>
+__device__ __forceinline__ void dftR(T2* v);
+
+// R = A * B in two levels (the dft8 / dft16 pattern): n = B n1 + n2, k = k1 + A k2; A-point DFTs
+// over n1, twiddles W_R^(n2 k1), B-point DFTs over n2
+template <int A, int B, bool INV, typename T2>
+__device__ __forceinline__ void dft_ab(T2* v) {
+  using T = decltype(v[0].x);
+  constexpr int R = A * B;
+  T2 a[B][A];
+#pragma unroll
+  for (int n2 = 0; n2 < B; ++n2) {
+#pragma unroll
+    for (int n1 = 0; n1 < A; ++n1) a[n2][n1] = v[B * n1 + n2];
+    dftR<A, INV>(a[n2]);
+  }
+#pragma unroll
+  for (int n2 = 1; n2 < B; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < A; ++k1) {
+      const int m = (n2 * k1) % R;
+      const T2 w{static_cast<T>(RootTable<R>::c[m]), static_cast<T>((INV ? 1.0 : -1.0) * RootTable<R>::s[m])};
+      a[n2][k1] = cmul(a[n2][k1], w);
+    }
+#pragma unroll
+  for (int k1 = 0; k1 < A; ++k1) {
+    T2 b[B];
+#pragma unroll
+    for (int n2 = 0; n2 < B; ++n2) b[n2] = a[n2][k1];
+    dftR<B, INV>(b);
+#pragma unroll
+    for (int k2 = 0; k2 < B; ++k2) v[k1 + A * k2] = b[k2];
+  }
+}
+
 template <int R, bool INV, typename T2>
 __device__ __forceinline__ void dftR(T2* v) {
   if constexpr (R == 2) dft2<INV>(v);
+  else if constexpr (R == 3) dft3<INV>(v);
   else if constexpr (R == 4) dft4<INV>(v);
+  else if constexpr (R == 5) dft5<INV>(v);
+  else if constexpr (R == 6) dft_ab<3, 2, INV>(v);
   else if constexpr (R == 8) dft8<INV>(v);
-  else dft16<INV>(v);
+  else if constexpr (R == 10) dft_ab<5, 2, INV>(v);
+  else if constexpr (R == 12) dft_ab<4, 3, INV>(v);
+  else {
+    static_assert(R == 16, "unsupported radix");
+    dft16<INV>(v);
+  }
 }
 
-// radix plan: 16 first, then 16, then the remainder
+// radix plan: 16 first, then 16 or the rest, the odd factor (3 or 5, possibly inside a 6, 10 or
+// 12) in the last pass.  Host and device share this function (twiddle tables, kernels).
+struct Radices {
+  int r0, r1, r2;
+};
+__host__ __device__ constexpr bool fft_radix_ok(int r) {
+  return r == 1 || r == 2 || r == 3 || r == 4 || r == 5 || r == 6 || r == 8 || r == 10 || r == 12 || r == 16;
+}
+__host__ __device__ constexpr Radices fft_radices(int n) {
+  if (n <= 16) return Radices{n, 1, 1};
+  const int rem = n / 16;
+  if (n % 16 != 0) return Radices{0, 0, 0};
+  if (fft_radix_ok(rem)) return Radices{16, rem, 1};
+  if (rem % 16 == 0 && fft_radix_ok(rem / 16)) return Radices{16, 16, rem / 16};
+  const int odd = rem % 3 == 0 ? 3 : (rem % 5 == 0 ? 5 : 1);
+  if (odd > 1 && fft_radix_ok(rem / odd)) return Radices{16, rem / odd, odd};
+  return Radices{0, 0, 0};
+}
+__host__ __device__ constexpr bool fft_length_ok(int n) {
+  const Radices r = fft_radices(n);
+  return n >= 2 && r.r0 > 0 && fft_radix_ok(r.r0) && fft_radix_ok(r.r1) && fft_radix_ok(r.r2) && r.r0 * r.r1 * r.r2 == n;
+}
+
 template <int N>
 struct FftPlan {
-  static constexpr int L = ilog2(N);
-  static constexpr int R0 = N >= 16 ? 16 : N;
-  static constexpr int R1 = N >= 256 ? 16 : (N / R0 > 1 ? N / R0 : 1);
-  static constexpr int R2 = N / (R0 * R1) > 1 ? N / (R0 * R1) : 1;
-  static_assert(R0 * R1 * R2 == N, "unsupported FFT length");
-  static_assert(R2 <= 16, "FFT length too large");
+  static constexpr Radices RR = fft_radices(N);
+  static constexpr int R0 = RR.r0;
+  static constexpr int R1 = RR.r1;
+  static constexpr int R2 = RR.r2;
+  static_assert(fft_length_ok(N), "unsupported FFT length");
   // per-pass twiddle tables, [r-1][k] (k = butterfly phase, fastest): for a fixed r the lanes of a
   // wave read consecutive entries, which is bank-conflict free (the former single W_N^m table
   // was read at k*r*stride, up to 16-way conflicts for even r)
@@ -215,17 +336,13 @@ struct FftPlan {
 
 // host-side table builder: entry [(r-1)*NS + k] of a pass = W_N^(k*r*N/(R*NS)) = exp(-2 pi i ...)
 inline int fft_twiddle_size(int n) {
-  int r0 = n >= 16 ? 16 : n;
-  int r1 = n >= 256 ? 16 : (n / r0 > 1 ? n / r0 : 1);
-  int r2 = n / (r0 * r1) > 1 ? n / (r0 * r1) : 1;
-  int t = (r1 > 1 ? (r1 - 1) * r0 : 0) + (r2 > 1 ? (r2 - 1) * r0 * r1 : 0);
+  const Radices r = fft_radices(n);
+  int t = (r.r1 > 1 ? (r.r1 - 1) * r.r0 : 0) + (r.r2 > 1 ? (r.r2 - 1) * r.r0 * r.r1 : 0);
   return t > 0 ? t : 1;
 }
 template <typename F>
 inline void fft_twiddle_fill(int n, F&& put) {  // put(index, m): entry index holds W_n^m
-  int r0 = n >= 16 ? 16 : n;
-  int r1 = n >= 256 ? 16 : (n / r0 > 1 ? n / r0 : 1);
-  int r2 = n / (r0 * r1) > 1 ? n / (r0 * r1) : 1;
+  const Radices rr = fft_radices(n);
   int off = 0;
   auto pass = [&](int R, int NS) {
     const int stride = n / (R * NS);
@@ -233,8 +350,8 @@ inline void fft_twiddle_fill(int n, F&& put) {  // put(index, m): entry index ho
       for (int k = 0; k < NS; ++k) put(off + (r - 1) * NS + k, k * r * stride);
     off += (R - 1) * NS;
   };
-  if (r1 > 1) pass(r1, r0);
-  if (r2 > 1) pass(r2, r0 * r1);
+  if (rr.r1 > 1) pass(rr.r1, rr.r0);
+  if (rr.r2 > 1) pass(rr.r2, rr.r0 * rr.r1);
 }
 
 // ---- real-signal forward transform of the z stage (N = 1024, 2048) -------------------------
@@ -323,7 +440,7 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
     const int idx = lane + b * TPR;
     if (NB % TPR == 0 || idx < NB) {
       const int row = idx / Q, j = idx - row * Q;
-      const int k = j & (NS - 1);
+      const int k = j % NS;
       if constexpr (NS > 1) {
 #pragma unroll
         for (int r = 1; r < R; ++r) {

@@ -227,7 +227,8 @@ class Solver {
   bool comm_warm_ = false;
   std::thread ckpt_thread_;
   std::exception_ptr ckpt_error_;
-  long ckpt_serial_ = 0;  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
+  long ckpt_serial_ = 0;
+  unsigned long long run_nonce_ = 0;  // same on every rank of one run (from the communicator id): checkpoint markers  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
 
   // rollback snapshot
   void* snap_ = nullptr;

@@ -6,11 +6,21 @@
 //   1. each lane eliminates its R-1 interior rows (Thomas, fp64), expressing them through the
 //      separator rows of its own and its left neighbour (the lane's last row is a separator);
 //   2. the 64 separator unknowns form a tridiagonal system across lanes, solved by parallel cyclic
-//      reduction (6 levels of cross-lane exchange in the VALU: DPP and permlane swaps);
+//      reduction (6 levels of cross-lane exchange, strides 1..32);
 //   3. each lane back-substitutes its interior rows.
 // The factorisation (elimination multipliers + PCR multipliers) is separated from the solve so
 // that several right-hand sides share one factorisation (complex data = 2 real RHS; the implicit
 // phi/omega solves share one; the influence-matrix homogeneous solutions add 2 more).
+//
+// Cross-lane exchange policies (template parameter XM):
+//   kXlBperm  ds_bpermute for every stride (LDS crossbar, no LDS storage)
+//   kXlDpp    VALU only: DPP wave_shr/shl, row_shr/shl/ror and v_permlane16/32_swap
+//   kXlLds    strides 1, 2 by DPP; strides >= 4 by one ds_write_b64 + two ds_read_b64 per value
+//             through a per-wave LDS scratch line.  The DPP forms of the long strides cost 11-22
+//             VALU instructions per double (8 of them v_cndmask) against 3 LDS instructions, and
+//             the LDS pipe runs beside the VALU.  Out-of-range neighbours read a clamped lane:
+//             the PCR multipliers that consume them are exactly zero there (A = 0 on lanes < s,
+//             C = 0 on lanes >= 64 - s at level s), so the results equal the zero-filled forms.
 //
 // This replaces the reference's cusparseZgtsvStridedBatch + per-call diagonal kernels
 // (derivatives_nu_double.cu:209-285, 390-415; hemholzt_nu_double.cu:98-251;
@@ -26,6 +36,9 @@ namespace dev {
 
 constexpr int kWave = 64;
 constexpr int kPcrLevels = 6;  // log2(64)
+constexpr int kXlBperm = 0, kXlDpp = 1, kXlLds = 2;
+// doubles of per-wave LDS scratch the kXlLds policy needs for K values exchanged at once
+constexpr int xl_scratch_doubles(int kmax) { return kmax * kWave; }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -41,15 +54,11 @@ __device__ __forceinline__ float bperm(float v, int src_lane) {
 }
 
 // ---- cross-lane shifts in the VALU (no LDS) -------------------------------------------------
-// The solver's communication is fixed-stride shifts (PCR strides 1..32, halos, wave sums).  A
-// ds_bpermute is an LDS round trip (~100+ cycles) on the dependent chain of every PCR level and,
-// at one wave per SIMD, nothing hides it; it also competes with the staging tiles for LDS.  Here:
 //   stride 1      DPP wave_shr:1 / wave_shl:1 (one VALU op per dword)
 //   stride 2, 4   chains of stride-1 DPP moves
 //   stride 8      DPP row_shr/row_shl inside 16-lane rows + row_ror fed through a 16-lane shift
 //   stride 16     v_permlane16_swap + v_permlane32_swap (CDNA4), both directions at once
 //   stride 32     v_permlane32_swap, both directions at once
-// XV = false selects the ds_bpermute versions (kernels that spill VGPRs keep them: see xl_valu()).
 constexpr int kDppRowShl = 0x100, kDppRowShr = 0x110, kDppRowRor = 0x120, kDppWaveShl1 = 0x130,
               kDppWaveShr1 = 0x138;
 template <int CTRL>
@@ -67,7 +76,7 @@ __device__ __forceinline__ void xl_updn16(int f, int& up, int& dn) {
 }
 // v of lane-S (0 for lanes < S) and of lane+S (0 for lanes >= 64-S); S is a compile-time constant
 // after unrolling at every call site
-__device__ __forceinline__ void xl_updn(int v, int s, int& up, int& dn) {
+__device__ __forceinline__ void xl_updn_i(int v, int s, int& up, int& dn) {
   const int lane = __lane_id(), l16 = lane & 15;
   switch (s) {
     case 1:
@@ -100,43 +109,80 @@ __device__ __forceinline__ void xl_updn(int v, int s, int& up, int& dn) {
     }
   }
 }
-template <bool XV>
-__device__ __forceinline__ void xl_updn(double v, int s, double& up, double& dn) {
-  if constexpr (!XV) {
-    const int lane = __lane_id();
-    const double u = bperm(v, (lane - s) & 63), d = bperm(v, (lane + s) & 63);
-    up = lane >= s ? u : 0.0;
-    dn = lane + s < 64 ? d : 0.0;
+__device__ __forceinline__ void xl_updn_dpp(double v, int s, double& up, double& dn) {
+  int ul, uh, dl, dh;
+  xl_updn_i(__double2loint(v), s, ul, dl);
+  xl_updn_i(__double2hiint(v), s, uh, dh);
+  up = __hiloint2double(uh, ul);
+  dn = __hiloint2double(dh, dl);
+}
+__device__ __forceinline__ void xl_updn_bperm(double v, int s, double& up, double& dn) {
+  const int lane = __lane_id();
+  const double u = bperm(v, (lane - s) & 63), d = bperm(v, (lane + s) & 63);
+  up = lane >= s ? u : 0.0;
+  dn = lane + s < 64 ? d : 0.0;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  return __hiloint2double(dpp_z<CTRL>(__double2hiint(v)), dpp_z<CTRL>(__double2loint(v)));
+}
+// value of lane-1 (0 in lane 0) / lane+1 (0 in lane 63): one DPP move per dword in every policy
+// except kXlBperm
+template <int XM>
+__device__ __forceinline__ double shfl_up1(double v) {
+  if constexpr (XM == kXlBperm) {
+    double u, d;
+    xl_updn_bperm(v, 1, u, d);
+    return u;
   } else {
-    int ul, uh, dl, dh;
-    xl_updn(__double2loint(v), s, ul, dl);
-    xl_updn(__double2hiint(v), s, uh, dh);
-    up = __hiloint2double(uh, ul);
-    dn = __hiloint2double(dh, dl);
+    return dpp_d<kDppWaveShr1>(v);
   }
 }
-// value of lane-s (0 for lanes < s)
-template <bool XV>
-__device__ __forceinline__ double shfl_up_z(double v, int s, int lane) {
-  if constexpr (XV) {
-    if (s == 1)
-      return __hiloint2double(dpp_z<kDppWaveShr1>(__double2hiint(v)), dpp_z<kDppWaveShr1>(__double2loint(v)));
+template <int XM>
+__device__ __forceinline__ double shfl_dn1(double v) {
+  if constexpr (XM == kXlBperm) {
+    double u, d;
+    xl_updn_bperm(v, 1, u, d);
+    return d;
+  } else {
+    return dpp_d<kDppWaveShl1>(v);
   }
-  double up, dn;
-  xl_updn<XV>(v, s, up, dn);
-  return up;
 }
-// value of lane+s (0 for lanes >= 64-s)
-template <bool XV>
-__device__ __forceinline__ double shfl_down_z(double v, int s, int lane) {
-  if constexpr (XV) {
-    if (s == 1)
-      return __hiloint2double(dpp_z<kDppWaveShl1>(__double2hiint(v)), dpp_z<kDppWaveShl1>(__double2loint(v)));
+
+// Cross-lane exchange of K values at stride s.  kXlLds: buf = this wave's scratch (K*64 doubles);
+// the neighbours outside the wave are clamped reads (see the header comment), the DPP/bpermute
+// forms zero-fill them.
+template <int XM>
+struct Xl {
+  double* buf = nullptr;
+  template <int K>
+  __device__ __forceinline__ void updn(const double (&v)[K], int s, double (&up)[K], double (&dn)[K]) const {
+    if constexpr (XM == kXlLds) {
+      if (s >= 4) {
+        const int lane = __lane_id();
+#pragma unroll
+        for (int k = 0; k < K; ++k) buf[k * kWave + lane] = v[k];
+        // a wave's LDS instructions execute in order: the reads below see these writes, and the
+        // next exchange's writes cannot overtake them (the compiler keeps the aliasing order)
+        const int lu = lane >= s ? lane - s : lane;
+        const int ld = lane + s < kWave ? lane + s : lane;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          up[k] = buf[k * kWave + lu];
+          dn[k] = buf[k * kWave + ld];
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if constexpr (XM == kXlBperm) xl_updn_bperm(v[k], s, up[k], dn[k]);
+      else xl_updn_dpp(v[k], s, up[k], dn[k]);
+    }
   }
-  double up, dn;
-  xl_updn<XV>(v, s, up, dn);
-  return dn;
-}
+};
+
 // 1/x to full double precision: hardware reciprocal estimate + two Newton steps (each doubles the
 // correct bits).  Replaces IEEE division (~10 dependent instructions incl. scale/fixup) on the
 // sequential factorisation chains; pivots here are O(1) and never denormal or zero.
@@ -149,9 +195,9 @@ __device__ __forceinline__ double fast_rcp(double x) {
 }
 
 // value of lane src_lane (wave-uniform) in every lane
-template <bool XV>
+template <int XM>
 __device__ __forceinline__ double bcast(double v, int src_lane) {
-  if constexpr (!XV)
+  if constexpr (XM == kXlBperm)
     return bperm(v, src_lane);
   else
     return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), src_lane),
@@ -160,10 +206,6 @@ __device__ __forceinline__ double bcast(double v, int src_lane) {
 
 // sum over the wave, bitwise identical in every lane: rotations inside 16-lane rows (each lane
 // pairs with a partner that forms the same sum), then the row pairs and halves via permlane swaps
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-  return __hiloint2double(dpp_z<CTRL>(__double2hiint(v)), dpp_z<CTRL>(__double2loint(v)));
-}
 __device__ __forceinline__ double xl_swap16(double v) {  // value of lane ^ 16
   const int row = __lane_id() >> 4;
   const auto ph = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
@@ -181,7 +223,7 @@ __device__ __forceinline__ double xl_swap32(double v) {  // value of lane ^ 32
 struct YTab {
   const double* d1_lo;   // D1 LHS (incl. wall closure rows)
   const double* d1_up;
-  const double* d1_rm;   // D1 RHS stencil, interior rows (0 on walls/pad)
+  const double* d1_rm;   // D1 RHS stencil B1: interior rows, wall closures folded in at rows 0, N-1
   const double* d1_rc;
   const double* d1_rp;
   const double* m_lo;    // compact D2 mass matrix M (interior rows)
@@ -190,26 +232,60 @@ struct YTab {
   const double* k_c;
   const double* k_up;
   const double* mask;    // 1 on interior rows, 0 on walls and padding
-  const double* trap;    // trapezoid weights (0 on padding)
-  const double* d1fac;   // D1 factorisation table [nf][64]
   const double* d1row0;  // first row of the dense D1 = A1^-1 B1 (wall derivative at y=-1)
   const double* d1rowN;  // last row (wall derivative at y=+1)
-  double w0[3], wN[3];   // D1 wall closures
+  const double* d1fac;   // D1 factorisation table [nf][64]
+  const double* trap;    // trapezoid weights (0 on padding; mean line only, never staged in LDS)
+  double w0[3], wN[3];   // D1 wall closures (w0[2], wN[2]: the third points, see d1_rhs)
   int N;
 };
+// The table buffer (YTablesDev::upload) is contiguous: kYTabRowTables per-row tables of 64*R
+// doubles in the YTab field order d1_lo .. d1rowN, then d1fac, then trap.
+constexpr int kYTabRowTables = 13;
 
 __device__ __forceinline__ double tab(const double* __restrict__ p, int r, int lane) {
   return p[r * 64 + lane];
 }
 
+// ---- factorisations: registers (k-dependent) or a 64-lane table (the constant D1) -------------
+// Per lane: the interior Thomas multipliers (inv, cp) of rows 0..R-2, the spikes Ls / Us (the
+// interior rows' responses to the left neighbour's and to the own separator unknown), the
+// separator row's coupling (as, cs), the PCR multipliers and the final pivot.
 template <int R>
 struct PFac {
   static constexpr int NI = (R > 1 ? R - 1 : 1);
-  double inv[NI], cp[NI];
-  double a0, cR2, as, cs;
-  double k1[kPcrLevels], k2[kPcrLevels];
-  double invB;
-  static constexpr int kNumFields = 2 * NI + 4 + 2 * kPcrLevels + 1;
+  double inv_[NI], cp_[NI], ls_[NI], us_[NI];
+  double as_, cs_;
+  double k1_[kPcrLevels], k2_[kPcrLevels];
+  double invB_;
+  static constexpr int kNumFields = 4 * NI + 2 + 2 * kPcrLevels + 1;
+  __device__ __forceinline__ double inv(int r) const { return inv_[r]; }
+  __device__ __forceinline__ double cp(int r) const { return cp_[r]; }
+  __device__ __forceinline__ double ls(int r) const { return ls_[r]; }
+  __device__ __forceinline__ double us(int r) const { return us_[r]; }
+  __device__ __forceinline__ double as() const { return as_; }
+  __device__ __forceinline__ double cs() const { return cs_; }
+  __device__ __forceinline__ double k1(int t) const { return k1_[t]; }
+  __device__ __forceinline__ double k2(int t) const { return k2_[t]; }
+  __device__ __forceinline__ double invB() const { return invB_; }
+};
+// the same fields read from the table written by pfac_store (field f of lane l at p[f*64 + l]):
+// no registers held across the solve
+template <int R>
+struct TFac {
+  static constexpr int NI = PFac<R>::NI;
+  const double* __restrict__ p;
+  int lane;
+  __device__ __forceinline__ double at(int f) const { return p[f * 64 + lane]; }
+  __device__ __forceinline__ double inv(int r) const { return at(r); }
+  __device__ __forceinline__ double cp(int r) const { return at(NI + r); }
+  __device__ __forceinline__ double ls(int r) const { return at(2 * NI + r); }
+  __device__ __forceinline__ double us(int r) const { return at(3 * NI + r); }
+  __device__ __forceinline__ double as() const { return at(4 * NI); }
+  __device__ __forceinline__ double cs() const { return at(4 * NI + 1); }
+  __device__ __forceinline__ double k1(int t) const { return at(4 * NI + 2 + t); }
+  __device__ __forceinline__ double k2(int t) const { return at(4 * NI + 2 + kPcrLevels + t); }
+  __device__ __forceinline__ double invB() const { return at(4 * NI + 2 + 2 * kPcrLevels); }
 };
 
 // ---- coefficient providers: abc(r, a, b, c) and a(r) for row j = lane*R + r ----------------
@@ -253,172 +329,138 @@ struct CoefHelm {
 };
 
 // ---- factorisation -----------------------------------------------------------------------
-template <int R, bool XV, class Coef>
-__device__ void pfactor(PFac<R>& F, const Coef& coef, int lane) {
+template <int R, int XM, class Coef>
+__device__ void pfactor(PFac<R>& F, const Coef& coef, const Xl<XM>& xl, int lane) {
   double A, B, C;
   if constexpr (R == 1) {
     coef.abc(0, A, B, C);
-    F.a0 = 0.0; F.cR2 = 0.0; F.as = A; F.cs = C;
-    F.inv[0] = 1.0; F.cp[0] = 0.0;
+    F.as_ = A; F.cs_ = C;
+    F.inv_[0] = 1.0; F.cp_[0] = 0.0; F.ls_[0] = 0.0; F.us_[0] = 0.0;
   } else {
-    double pc = 0.0;
+    double pc = 0.0, a0 = 0.0, cR2 = 0.0;
 #pragma unroll
     for (int r = 0; r < R - 1; ++r) {
       double a, b, c;
       coef.abc(r, a, b, c);
-      if (r == 0) F.a0 = a;
-      if (r == R - 2) F.cR2 = c;
+      if (r == 0) a0 = a;
+      if (r == R - 2) cR2 = c;
       const double den = b - a * pc;
-      F.inv[r] = fast_rcp(den);
-      F.cp[r] = c * F.inv[r];
-      pc = F.cp[r];
+      F.inv_[r] = fast_rcp(den);
+      F.cp_[r] = c * F.inv_[r];
+      pc = F.cp_[r];
     }
-    // left spike L (rhs = -a0 e_0) and right spike U (rhs = -cR2 e_{R-2})
-    double dl[R - 1];
-    dl[0] = -F.a0 * F.inv[0];
+    // left spike (interior response to the left separator: rhs -a0 e_0) and right spike (to the
+    // own separator: rhs -cR2 e_{R-2}), both fully back-substituted
+    F.ls_[0] = -a0 * F.inv_[0];
 #pragma unroll
-    for (int r = 1; r < R - 1; ++r) dl[r] = -coef.a(r) * dl[r - 1] * F.inv[r];
-    const double L_last = dl[R - 2];
-    double Lr = dl[R - 2];
+    for (int r = 1; r < R - 1; ++r) F.ls_[r] = -coef.a(r) * F.ls_[r - 1] * F.inv_[r];
 #pragma unroll
-    for (int r = R - 3; r >= 0; --r) Lr = dl[r] - F.cp[r] * Lr;
-    const double L_first = Lr;
-    const double U_last = -F.cR2 * F.inv[R - 2];
-    double Ur = U_last;
+    for (int r = R - 3; r >= 0; --r) F.ls_[r] -= F.cp_[r] * F.ls_[r + 1];
+    F.us_[R - 2] = -cR2 * F.inv_[R - 2];
 #pragma unroll
-    for (int r = R - 3; r >= 0; --r) Ur = -F.cp[r] * Ur;
-    const double U_first = Ur;
+    for (int r = R - 3; r >= 0; --r) F.us_[r] = -F.cp_[r] * F.us_[r + 1];
     double as, bs, cs;
     coef.abc(R - 1, as, bs, cs);
-    F.as = as;
-    F.cs = cs;
-    const double L0n = shfl_down_z<XV>(L_first, 1, lane);
-    const double U0n = shfl_down_z<XV>(U_first, 1, lane);
-    A = as * L_last;
-    B = bs + as * U_last + cs * L0n;
+    F.as_ = as;
+    F.cs_ = cs;
+    const double L0n = shfl_dn1<XM>(F.ls_[0]);
+    const double U0n = shfl_dn1<XM>(F.us_[0]);
+    A = as * F.ls_[R - 2];
+    B = bs + as * F.us_[R - 2] + cs * L0n;
     C = cs * U0n;
   }
 #pragma unroll
   for (int t = 0; t < kPcrLevels; ++t) {
     const int s = 1 << t;
     // each lane inverts its own pivot once and the neighbours receive 1/B (one reciprocal per
-    // level instead of two divisions)
-    const double iB = fast_rcp(B);
-    double Am, iBm, Cm, Ap, iBp, Cp;
-    xl_updn<XV>(A, s, Am, Ap);
-    xl_updn<XV>(iB, s, iBm, iBp);
-    xl_updn<XV>(C, s, Cm, Cp);
-    const bool hm = lane >= s, hp = lane + s < 64;
-    const double k1 = hm ? A * iBm : 0.0;
-    const double k2 = hp ? C * iBp : 0.0;
-    const double nA = -Am * k1;
-    const double nC = -Cp * k2;
-    const double nB = B - Cm * k1 - Ap * k2;
+    // level instead of two divisions).  A is exactly 0 on lanes < s and C on lanes >= 64 - s, so
+    // the multipliers vanish there whatever the (zero-filled or clamped) neighbour values are.
+    const double v[3] = {A, fast_rcp(B), C};
+    double m[3], p[3];
+    xl.template updn<3>(v, s, m, p);
+    const double k1 = A * m[1];
+    const double k2 = C * p[1];
+    const double nA = -m[0] * k1;
+    const double nC = -p[2] * k2;
+    const double nB = B - m[2] * k1 - p[0] * k2;
     A = nA; B = nB; C = nC;
-    F.k1[t] = k1;
-    F.k2[t] = k2;
+    F.k1_[t] = k1;
+    F.k2_[t] = k2;
   }
-  F.invB = fast_rcp(B);
+  F.invB_ = fast_rcp(B);
 }
 
 template <int R>
 __device__ void pfac_store(const PFac<R>& F, double* __restrict__ out, int lane) {
+  constexpr int NI = PFac<R>::NI;
   int f = 0;
 #pragma unroll
-  for (int r = 0; r < PFac<R>::NI; ++r) out[(f++) * 64 + lane] = F.inv[r];
+  for (int r = 0; r < NI; ++r) out[(f++) * 64 + lane] = F.inv_[r];
 #pragma unroll
-  for (int r = 0; r < PFac<R>::NI; ++r) out[(f++) * 64 + lane] = F.cp[r];
-  out[(f++) * 64 + lane] = F.a0;
-  out[(f++) * 64 + lane] = F.cR2;
-  out[(f++) * 64 + lane] = F.as;
-  out[(f++) * 64 + lane] = F.cs;
+  for (int r = 0; r < NI; ++r) out[(f++) * 64 + lane] = F.cp_[r];
 #pragma unroll
-  for (int t = 0; t < kPcrLevels; ++t) out[(f++) * 64 + lane] = F.k1[t];
+  for (int r = 0; r < NI; ++r) out[(f++) * 64 + lane] = F.ls_[r];
 #pragma unroll
-  for (int t = 0; t < kPcrLevels; ++t) out[(f++) * 64 + lane] = F.k2[t];
-  out[(f++) * 64 + lane] = F.invB;
+  for (int r = 0; r < NI; ++r) out[(f++) * 64 + lane] = F.us_[r];
+  out[(f++) * 64 + lane] = F.as_;
+  out[(f++) * 64 + lane] = F.cs_;
+#pragma unroll
+  for (int t = 0; t < kPcrLevels; ++t) out[(f++) * 64 + lane] = F.k1_[t];
+#pragma unroll
+  for (int t = 0; t < kPcrLevels; ++t) out[(f++) * 64 + lane] = F.k2_[t];
+  out[(f++) * 64 + lane] = F.invB_;
 }
 
-template <int R>
-__device__ void pfac_load(PFac<R>& F, const double* __restrict__ in, int lane) {
-  int f = 0;
-#pragma unroll
-  for (int r = 0; r < PFac<R>::NI; ++r) F.inv[r] = in[(f++) * 64 + lane];
-#pragma unroll
-  for (int r = 0; r < PFac<R>::NI; ++r) F.cp[r] = in[(f++) * 64 + lane];
-  F.a0 = in[(f++) * 64 + lane];
-  F.cR2 = in[(f++) * 64 + lane];
-  F.as = in[(f++) * 64 + lane];
-  F.cs = in[(f++) * 64 + lane];
-#pragma unroll
-  for (int t = 0; t < kPcrLevels; ++t) F.k1[t] = in[(f++) * 64 + lane];
-#pragma unroll
-  for (int t = 0; t < kPcrLevels; ++t) F.k2[t] = in[(f++) * 64 + lane];
-  F.invB = in[(f++) * 64 + lane];
-}
-
-// ---- solve K right-hand sides in place ----------------------------------------------------
-template <int R, int K, bool XV, class Coef>
-__device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], int lane) {
+// ---- solve K right-hand sides in place (F: PFac in registers or TFac from a table) -----------
+// SPIKE form: interior Thomas in place, the separator system by PCR, then every interior row adds
+// its two spike responses (two independent FMAs per row instead of a second elimination pass).
+template <int R, int K, int XM, class Fac, class Coef>
+__device__ void psolve(const Fac& F, const Coef& coef, double (&d)[K][R], const Xl<XM>& xl, int lane) {
   double D[K];
   if constexpr (R == 1) {
 #pragma unroll
     for (int k = 0; k < K; ++k) D[k] = d[k][0];
   } else {
-    double P0[K], PL[K];
     {
-      double dp[K][R - 1];
+      const double i0 = F.inv(0);
 #pragma unroll
-      for (int k = 0; k < K; ++k) dp[k][0] = d[k][0] * F.inv[0];
-#pragma unroll
-      for (int r = 1; r < R - 1; ++r) {
-        const double a = coef.a(r);
-#pragma unroll
-        for (int k = 0; k < K; ++k) dp[k][r] = (d[k][r] - a * dp[k][r - 1]) * F.inv[r];
-      }
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        double P = dp[k][R - 2];
-        PL[k] = P;
-#pragma unroll
-        for (int r = R - 3; r >= 0; --r) P = dp[k][r] - F.cp[r] * P;
-        P0[k] = P;
-      }
+      for (int k = 0; k < K; ++k) d[k][0] *= i0;
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) D[k] = d[k][R - 1] - F.as * PL[k] - F.cs * shfl_down_z<XV>(P0[k], 1, lane);
+    for (int r = 1; r < R - 1; ++r) {
+      const double a = coef.a(r), ir = F.inv(r);
+#pragma unroll
+      for (int k = 0; k < K; ++k) d[k][r] = (d[k][r] - a * d[k][r - 1]) * ir;
+    }
+#pragma unroll
+    for (int r = R - 3; r >= 0; --r) {
+      const double c = F.cp(r);
+#pragma unroll
+      for (int k = 0; k < K; ++k) d[k][r] -= c * d[k][r + 1];
+    }
+    const double as = F.as(), cs = F.cs();
+#pragma unroll
+    for (int k = 0; k < K; ++k) D[k] = d[k][R - 1] - as * d[k][R - 2] - cs * shfl_dn1<XM>(d[k][0]);
   }
 #pragma unroll
   for (int t = 0; t < kPcrLevels; ++t) {
     const int s = 1 << t;
+    double Dm[K], Dp[K];
+    xl.template updn<K>(D, s, Dm, Dp);
+    const double k1 = F.k1(t), k2 = F.k2(t);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      double Dm, Dp;
-      xl_updn<XV>(D[k], s, Dm, Dp);
-      D[k] = D[k] - F.k1[t] * Dm - F.k2[t] * Dp;
-    }
+    for (int k = 0; k < K; ++k) D[k] = D[k] - k1 * Dm[k] - k2 * Dp[k];
   }
+  const double invB = F.invB();
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double y = D[k] * F.invB;
+    const double y = D[k] * invB;
     if constexpr (R == 1) {
       d[k][0] = y;
     } else {
-      const double yl = shfl_up_z<XV>(y, 1, lane);
-      d[k][0] -= F.a0 * yl;
-      d[k][R - 2] -= F.cR2 * y;
-      // interior solve with the separator values known
-      double dp[R - 1];
-      dp[0] = d[k][0] * F.inv[0];
+      const double yl = shfl_up1<XM>(y);
 #pragma unroll
-      for (int r = 1; r < R - 1; ++r) dp[r] = (d[k][r] - coef.a(r) * dp[r - 1]) * F.inv[r];
-      double x = dp[R - 2];
-      d[k][R - 2] = x;
-#pragma unroll
-      for (int r = R - 3; r >= 0; --r) {
-        x = dp[r] - F.cp[r] * x;
-        d[k][r] = x;
-      }
+      for (int r = 0; r < R - 1; ++r) d[k][r] += yl * F.ls(r) + y * F.us(r);
       d[k][R - 1] = y;
     }
   }
@@ -426,31 +468,27 @@ __device__ void psolve(const PFac<R>& F, const Coef& coef, double (&d)[K][R], in
 
 // ---- stencils ----------------------------------------------------------------------------
 // value at global row j (wave-uniform j); returns 0 if j out of range
-template <int R, bool XV>
+template <int R, int XM>
 __device__ __forceinline__ double row_value(const double (&x)[R], int j, int lane) {
   const int src = j / R, rr = j - src * R;
   double v = 0.0;
 #pragma unroll
   for (int r = 0; r < R; ++r)
     if (r == rr) v = x[r];
-  return bcast<XV>(v, src);
+  return bcast<XM>(v, src);
 }
 
-template <int R, int K, bool XV>
-__device__ __forceinline__ void halo(const double (&x)[K][R], double (&left)[K], double (&right)[K], int lane) {
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    left[k] = shfl_up_z<XV>(x[k][R - 1], 1, lane);
-    right[k] = shfl_down_z<XV>(x[k][0], 1, lane);
-  }
-}
-
-// out = tridiag(lo, c, up) * x with per-row tables (c may be null => mask)
-template <int R, int K, bool XV>
+// out = tridiag(lo, c, up) * x with per-row tables (c = mask for M); cl, cc, cu scale the three
+// diagonals of a second table set added on top (fused (cA A + cB B) x, see apply_tri2)
+template <int R, int K, int XM>
 __device__ void apply_tri(const double* __restrict__ lo, const double* __restrict__ cc, const double* __restrict__ up,
                           const double (&x)[K][R], double (&out)[K][R], int lane) {
   double L[K], Rt[K];
-  halo<R, K, XV>(x, L, Rt, lane);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    L[k] = shfl_up1<XM>(x[k][R - 1]);
+    Rt[k] = shfl_dn1<XM>(x[k][0]);
+  }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const double a = tab(lo, r, lane), b = tab(cc, r, lane), c = tab(up, r, lane);
@@ -463,27 +501,80 @@ __device__ void apply_tri(const double* __restrict__ lo, const double* __restric
   }
 }
 
-// D1 right-hand side B1 f (interior stencil + 3-point one-sided wall closures)
-template <int R, int K, bool XV>
-__device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][R], int lane) {
-  apply_tri<R, K, XV>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane);
-  const int N = t.N;
-  const int jN = N - 1, lN = jN / R, rN = jN - lN * R;
+// out = (sA A + sB B) x for two tridiagonal table sets A = (alo, ac, aup), B = (blo, bc, bup)
+// (the explicit RK3 operator (1 - dt a nu k^2) M + dt a nu K in one pass, no M x / K x temporaries)
+template <int R, int K, int XM>
+__device__ void apply_tri2(const double* __restrict__ alo, const double* __restrict__ ac,
+                           const double* __restrict__ aup, double sA, const double* __restrict__ blo,
+                           const double* __restrict__ bc, const double* __restrict__ bup, double sB,
+                           const double (&x)[K][R], double (&out)[K][R], int lane) {
+  double L[K], Rt[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const double f1 = row_value<R, XV>(x[k], 1, lane), f2 = row_value<R, XV>(x[k], 2, lane);
-    const double g1 = row_value<R, XV>(x[k], N - 2, lane), g2 = row_value<R, XV>(x[k], N - 3, lane);
-    const double f0 = row_value<R, XV>(x[k], 0, lane), g0 = row_value<R, XV>(x[k], N - 1, lane);
-    if (lane == 0) out[k][0] = t.w0[0] * f0 + t.w0[1] * f1 + t.w0[2] * f2;
+    L[k] = shfl_up1<XM>(x[k][R - 1]);
+    Rt[k] = shfl_dn1<XM>(x[k][0]);
+  }
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-      if (lane == lN && r == rN) out[k][r] = t.wN[0] * g0 + t.wN[1] * g1 + t.wN[2] * g2;
+  for (int r = 0; r < R; ++r) {
+    const double a = sA * tab(alo, r, lane) + sB * tab(blo, r, lane);
+    const double b = sA * tab(ac, r, lane) + sB * tab(bc, r, lane);
+    const double c = sA * tab(aup, r, lane) + sB * tab(bup, r, lane);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double xm = (r == 0) ? L[k] : x[k][r - 1];
+      const double xp = (r == R - 1) ? Rt[k] : x[k][r + 1];
+      out[k][r] = a * xm + b * x[k][r] + c * xp;
+    }
   }
 }
 
-template <int K, bool XV>
+// D1 right-hand side B1 f: the 3-point interior stencil with the one-sided wall closures folded
+// into rows 0 and N-1 of the tables; the closures' third points are f_2 (row 0: lane 0's own
+// register when R >= 3) and f_{N-3} (row N-1 at the wave-uniform slot rN: one scalar branch)
+template <int R, int K, int XM>
+__device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][R], int lane) {
+  apply_tri<R, K, XM>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane);
+  const int N = t.N;
+  const int lN = (N - 1) / R, rN = (N - 1) - lN * R;  // wave-uniform
+  if constexpr (R >= 3) {
+    const double cp2 = lane == 0 ? t.w0[2] : 0.0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k][0] += cp2 * x[k][2];
+    const double cm2 = lane == lN ? t.wN[2] : 0.0;
+    switch (rN) {
+#define CH_D1_RM2(RR)                                                                  \
+  case RR:                                                                             \
+    if constexpr (RR < R) {                                                            \
+      _Pragma("unroll") for (int k = 0; k < K; ++k) {                                  \
+        const double xm2 = RR >= 2 ? x[k][RR >= 2 ? RR - 2 : 0]                        \
+                                   : shfl_up1<XM>(x[k][RR == 1 ? R - 1 : R - 2]);      \
+        out[k][RR] += cm2 * xm2;                                                       \
+      }                                                                                \
+    }                                                                                  \
+    break;
+      CH_D1_RM2(0) CH_D1_RM2(1) CH_D1_RM2(2) CH_D1_RM2(3) CH_D1_RM2(4) CH_D1_RM2(5) CH_D1_RM2(6)
+      CH_D1_RM2(7) CH_D1_RM2(8) CH_D1_RM2(9) CH_D1_RM2(10) CH_D1_RM2(11) CH_D1_RM2(12)
+      CH_D1_RM2(13) CH_D1_RM2(14) CH_D1_RM2(15) CH_D1_RM2(16) CH_D1_RM2(17) CH_D1_RM2(18)
+      CH_D1_RM2(19) CH_D1_RM2(20) CH_D1_RM2(21) CH_D1_RM2(22) CH_D1_RM2(23)
+#undef CH_D1_RM2
+      default: break;
+    }
+  } else {
+    // R <= 2 (NY <= 128): the closure points straddle lanes; broadcast them
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double f2 = row_value<R, XM>(x[k], 2, lane), g2 = row_value<R, XM>(x[k], N - 3, lane);
+      if (lane == 0) out[k][0] += t.w0[2] * f2;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (lane == lN && r == rN) out[k][r] += t.wN[2] * g2;
+    }
+  }
+}
+
+template <int K, int XM>
 __device__ __forceinline__ void wave_sum_n(double (&v)[K]) {
-  if constexpr (!XV) {
+  if constexpr (XM == kXlBperm) {
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1)
 #pragma unroll
@@ -504,11 +595,30 @@ __device__ __forceinline__ void wave_sum_n(double (&v)[K]) {
   for (int k = 0; k < K; ++k) v[k] += xl_swap32(v[k]);
 }
 
-template <int R, bool XV>
+template <int XM>
 __device__ __forceinline__ double wave_sum(double v) {
   double a[1] = {v};
-  wave_sum_n<1, XV>(a);
+  wave_sum_n<1, XM>(a);
   return a[0];
+}
+
+// ---- operators on whole lines ------------------------------------------------------------
+// out = D1 x (compact first derivative): B1 x, then the constant factorisation from its table
+template <int R, int K, int XM>
+__device__ __forceinline__ void d1_apply_to(const YTab& t, const double (&x)[K][R], double (&out)[K][R],
+                                            const Xl<XM>& xl, int lane) {
+  d1_rhs<R, K, XM>(t, x, out, lane);
+  const TFac<R> F{t.d1fac, lane};
+  const CoefD1 cd{t, lane};
+  psolve<R, K, XM>(F, cd, out, xl, lane);
+}
+template <int R, int K, int XM>
+__device__ __forceinline__ void apply_M(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
+  apply_tri<R, K, XM>(t.m_lo, t.mask, t.m_up, x, o, lane);
+}
+template <int R, int K, int XM>
+__device__ __forceinline__ void apply_K(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
+  apply_tri<R, K, XM>(t.k_lo, t.k_c, t.k_up, x, o, lane);
 }
 
 }  // namespace dev

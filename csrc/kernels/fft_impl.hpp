@@ -1,0 +1,977 @@
+// Transform stages between spectral and physical space (SURVEY §7.3 K-XB, K-PHYS, K-XF).
+//
+//  * xfft_backward: for each local y plane and a chunk of C kz columns, gather the retained kx
+//    modes (directly from the all-to-all receive blocks; zero-padded to NX in LDS), inverse C2C of
+//    length NX, write [y][x][kz].  Replaces the x-part of the reference's 2-D cufftExecC2R and the
+//    transposeYZX2XYZ local transposes + dealias (fft.c:54-78, channel_cuda_mpi.c:95-128).
+//  * zphys: per (y,x) row, the six fields u,v,w,wx,wy,wz are paired into three complex rows
+//    (z = a + i b), zero-padded from the retained kz to 2NZ-2 points, inverse FFT'd, the
+//    rotational nonlinear term H = u x omega is formed in registers (rotorkernel,
+//    convolution_kernels.cu:69-148) with the CFL maxima (the cublasIsamax calls of fft.c:143-200),
+//    and H is forward transformed (Hx+iHy and pairs of Hz rows) and truncated to the retained kz.
+//    Physical fields never leave LDS/registers.
+//  * xfft_forward: forward C2C along x and truncation to the retained kx, written straight into
+//    the per-destination all-to-all send blocks (or, for P=1, into the spectral H arrays).
+// Kernel templates of the transform stages; fft.hip holds the host API and the length dispatch,
+// fft_pow2.hip / fft_r3.hip / fft_r5.hip instantiate the kernels per length family (parallel
+// compilation).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <vector>
+
+#include "channel/common.hpp"
+#include "channel/fft_device.hpp"
+#include "channel/kernels.hpp"
+
+namespace channel {
+
+using namespace dev;
+
+constexpr int pow2_floor(int n) { return n < 2 ? 1 : 2 * pow2_floor(n / 2); }
+constexpr int pow2_ceil(int n) { return pow2_floor(n) < n ? 2 * pow2_floor(n) : pow2_floor(n); }
+
+// ---- x-direction -------------------------------------------------------------------------
+// fp64 at NX = 2048: 2 columns per tile (the 4-column tile plus the twiddles would exceed the
+// 160 KB of LDS), one wave per column
+constexpr int xcfg_c(int nx, int tsz) {
+  return tsz == 4 ? (nx > 512 ? 8 : 16) : (nx > 1024 ? 2 : (nx > 512 ? 4 : (nx >= 512 ? 8 : 16)));
+}
+// WIDE = 1: twice the kz columns per tile (128-B row segments) with 512 threads and one block per
+// CU (the same 8 waves per CU); WIDE = 0: 64-B segments, 256 threads, two blocks per CU.
+constexpr int xcfg_nt(int wide, int c = 4) { return wide ? 512 : (c >= 4 ? 256 : 64 * c); }
+constexpr int xcfg_minb(int wide) { return wide ? 1 : 2; }
+template <int NX, typename T, int WIDE = 0>
+struct XCfg {
+  // kz columns per tile
+  static constexpr int C = xcfg_c(NX, sizeof(T)) * (WIDE ? 2 : 1);
+  // fp32 at 2048 points: the LDS holds one 8-column tile per CU, so that tile gets 8 waves, two per
+  // row (TPR = 128, block barriers between the passes; 2 waves per SIMD without spills) instead of
+  // 4 waves of 2 rows at one wave per SIMD
+  // (fp64 from 1024 points likewise: 4 columns x 2 waves at 1024, 2 x 2 at 2048)
+  static constexpr bool BIG = NX >= (sizeof(T) == 4 ? 2048 : 1024) && !WIDE;
+  static constexpr int NT = BIG ? 128 * (C < 4 ? C : 4) : xcfg_nt(WIDE, C);
+  static constexpr int MINB = BIG ? 1 : xcfg_minb(WIDE);
+  static constexpr int TPR = BIG ? 128 : 64;  // threads per transformed row
+  // row pitch: padded FFT row + 1 or 2 slots so that the transposing global->LDS stores (lanes =
+  // C consecutive kz columns x consecutive x) hit distinct banks (pitch*c spreads over 16 slots)
+  static constexpr int PITCH = FftPitch<NX>::value + (sizeof(T) == 4 ? (C >= 16 ? 1 : 2) : (C >= 8 ? 1 : 2));
+};
+
+// CHANNEL_FFT_DIAG=1 skips the in-LDS transforms (timing diagnosis only: results are wrong)
+static int fft_diag() {
+  static const int d = [] {
+    const char* e = std::getenv("CHANNEL_FFT_DIAG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return d;
+}
+
+static bool xwide_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_XWIDE");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
+// Segment lookup in a small split table (at most MAXS segments) without dynamic indexing.
+// Indexing a by-value kernel-argument array with a per-lane index makes hipcc gather the entries
+// from the kernarg segment with per-lane global loads, each followed by s_waitcnt vmcnt(0): that
+// drained every in-flight prefetch load and store of the wave at every element and serialised
+// the x transforms.  Unrolled over the compile-time capacity the entries are wave-uniform
+// (SGPR) values and the lookup is a chain of compares and selects.
+struct SegPos {
+  int start;      // first index of the segment
+  int count;      // its length
+  long long off;  // element offset of its block
+  int idx;        // segment index
+};
+template <int MAXS = 8>
+__device__ __forceinline__ SegPos seg_find(const int* start, const long long* off, int n, int i) {
+  SegPos p{start[0], start[1] - start[0], off[0], 0};
+#pragma unroll
+  for (int q = 1; q < MAXS; ++q)
+    if (q < n && i >= start[q]) p = SegPos{start[q], start[q + 1] - start[q], off[q], q};
+  return p;
+}
+
+// Segment of i for i in the wave-uniform window [lo, lo + span) when every segment is at least
+// span long (checked on the host): the window meets at most two segments, found with scalar
+// lookups of its two ends, and each lane picks one with a single compare.
+template <int MAXS = 8>
+__device__ __forceinline__ SegPos seg_find_win(const int* start, const long long* off, int n, int lo, int span, int i) {
+  const SegPos a = seg_find<MAXS>(start, off, n, lo);
+  const SegPos b = seg_find<MAXS>(start, off, n, lo + span - 1);
+  return i >= b.start ? b : a;
+}
+// kx segment addressing of the x kernels: kSegOne = one block, no self block (one rank);
+// kSegWin = window lookup (seg_find_win); kSegFull = per-element lookup
+constexpr int kSegOne = 0, kSegWin = 1, kSegFull = 2;
+template <int NT, int C>
+inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
+  if (n == 1 && self_seg < 0 && off0 == 0) return kSegOne;
+  int m = 1 << 30;
+  for (int q = 0; q < n; ++q) m = std::min(m, start[q + 1] - start[q]);
+  return m >= NT / C ? kSegWin : kSegFull;
+}
+
+// Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
+// LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
+// into registers right after the current tile is staged into LDS, so they are in flight during
+// the FFT and the stores; one block per tile (the previous design) left HBM idle for most of each
+// block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
+// SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
+// compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
+    xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NX, T, WIDE>;
+  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
+  constexpr int NKMAX = 2 * (NX / 3) + 1;
+  constexpr int EPT = (NKMAX * C + NT - 1) / NT;
+  __shared__ T2 s[C * PITCH];
+  constexpr int TS = FftPlan<NX>::TSIZE;
+  __shared__ T2 tws[TS];
+  for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
+  const int nkzc = (a.nkz + C - 1) / C;
+  const int ntiles = a.ny * nkzc * a.nfields;
+  const int G = static_cast<int>(gridDim.x);
+  const int tid = threadIdx.x;
+  const int nload = a.nkx * C;
+  T2 v[EPT];
+  // tile t -> (f, y, kz0); at each iteration the blocks of one XCD take consecutive tiles
+  auto fetch = [&](int t) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
+    // this rank's own block is read in place from its spectral field (no self exchange)
+    const T2* sbase = src.self_seg >= 0 ? static_cast<const T2*>(src.self_base) + f * src.self_field_stride : base;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      // unconditional load from a clamped valid address: rows i >= nkx are never staged,
+      // columns kz >= nkz are transformed (independently) but never stored
+      const int i = min(e / C, a.nkx - 1);
+      const int kz = min(kz0 + e % C, a.nkz - 1);
+      if constexpr (SM == kSegOne) {
+        v[q] = base[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      } else {
+        const SegPos sp = SM == kSegWin ? seg_find_win(src.kx_start, src.off, src.nsrc, (q * NT) / C, NT / C, i)
+                                        : seg_find(src.kx_start, src.off, src.nsrc, i);
+        const T2* b = sp.idx == src.self_seg ? sbase : base;
+        // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
+        v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
+      }
+    }
+  };
+  int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  if (t < ntiles) fetch(t);
+  for (; t < ntiles; t += G) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    lds_barrier();  // previous tile's stores have finished reading s
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int i = e / C, c = e - i * C;
+      const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+      if (e < nload) s[c * PITCH + fft_pidx(x)] = v[q];
+    }
+    for (int e = tid; e < (NX - a.nkx) * C; e += NT) {
+      const int j = e / C, c = e - j * C;
+      s[c * PITCH + fft_pidx(a.Kx + 1 + j)] = T2{0, 0};
+    }
+    lds_barrier();
+    if (t + G < ntiles) fetch(t + G);
+    {
+      constexpr int TPR = Cfg::TPR;
+      constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
+      // one row at a time from 1024 points (the prefetched next tile already holds EPT registers);
+      // shorter rows RB at a time, so a radix-16 pass has 64 butterflies for the 64 lanes
+      // (a power of two, so it divides RW: the last call must not run into the next wave's rows)
+      constexpr int RB = pow2_floor(1024 / NX < 1 ? 1 : (1024 / NX < RW ? 1024 / NX : RW));
+      if (!(a.diag & 1))
+#pragma unroll 1
+        for (int rr = 0; rr < RW; rr += RB)
+          wave_fft<NX, RB, PITCH, true, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+    }
+    lds_barrier();
+    T2* out = phys + f * a.field_stride_phys;
+    for (int e = tid; e < NX * C; e += NT) {
+      const int x = e / C, c = e - x * C;
+      const int kz = kz0 + c;
+      if (kz < a.nkz) {
+        if constexpr (SEG) {
+          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+          out[sp.off + (static_cast<long long>(y) * sp.count + (x - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        } else {
+          out[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
+              s[c * PITCH + fft_pidx(x)];
+        }
+      }
+    }
+  }
+}
+
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
+__global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
+    xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NX, T, WIDE>;
+  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  constexpr int EPT = (NX * C + NT - 1) / NT;
+  __shared__ T2 s[C * PITCH];
+  constexpr int TS = FftPlan<NX>::TSIZE;
+  __shared__ T2 tws[TS];
+  for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
+  const int nkzc = (a.nkz + C - 1) / C;
+  const int ntiles = a.ny * nkzc * a.nfields;
+  const int G = static_cast<int>(gridDim.x);
+  const int tid = threadIdx.x;
+  T2 v[EPT];
+  auto fetch = [&](int t) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    const T2* in = phys + f * a.field_stride_phys;
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int x = min(e / C, NX - 1);
+      const int kz = min(kz0 + e % C, a.nkz - 1);
+      if constexpr (SEG) {
+        const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+        v[q] = in[static_cast<unsigned>(sp.off) +
+                  static_cast<unsigned>(y * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      } else {
+        v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+      }
+    }
+  };
+  int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  if (t < ntiles) fetch(t);
+  for (; t < ntiles; t += G) {
+    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
+    const int y = rest % a.ny, f = rest / a.ny;
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      const int x = e / C, c = e - x * C;
+      if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
+    }
+    lds_barrier();
+    if (t + G < ntiles) fetch(t + G);
+    {
+      constexpr int TPR = Cfg::TPR;
+      constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
+      // one row at a time from 1024 points (the prefetched next tile already holds EPT registers);
+      // shorter rows RB at a time, so a radix-16 pass has 64 butterflies for the 64 lanes
+      // (a power of two, so it divides RW: the last call must not run into the next wave's rows)
+      constexpr int RB = pow2_floor(1024 / NX < 1 ? 1 : (1024 / NX < RW ? 1024 / NX : RW));
+      if (!(a.diag & 1))
+#pragma unroll 1
+        for (int rr = 0; rr < RW; rr += RB)
+          wave_fft<NX, RB, PITCH, false, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+    }
+    lds_barrier();
+    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    // this rank's own block goes straight into its spectral field (no self exchange)
+    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
+    for (int e0 = 0; e0 < a.nkx * C; e0 += NT) {
+      const int e = e0 + tid;
+      const int i = e / C, c = e - i * C;
+      const int kz = kz0 + c;
+      if (e < a.nkx * C && kz < a.nkz) {
+        const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+        if constexpr (SM == kSegOne) {
+          outb[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
+              s[c * PITCH + fft_pidx(x)];
+        } else {
+          const SegPos sp = SM == kSegWin ? seg_find_win(dst.kx_start, dst.off, dst.ndst, e0 / C, NT / C, i)
+                                          : seg_find(dst.kx_start, dst.off, dst.ndst, i);
+          T2* ob = sp.idx == dst.self_seg ? soutb : outb;
+          ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+        }
+      }
+    }
+  }
+}
+
+template <int NN, typename T, int WIDE>
+static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NN, T, WIDE>;
+  // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
+  // its windows, computed up front, spilled ~640 SGPRs)
+  const int sm = seg_mode<Cfg::NT, Cfg::C>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
+  auto kern = a.npseg > 1     ? xfft_backward_kernel<NN, T, true, WIDE>
+              : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne>
+                              : xfft_backward_kernel<NN, T, false, WIDE, kSegFull>;
+  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
+}
+
+template <int NN, typename T, int WIDE>
+static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
+  using T2 = typename C2<T>::type;
+  using Cfg = XCfg<NN, T, WIDE>;
+  const int sm = seg_mode<Cfg::NT, Cfg::C>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
+  auto kern = a.npseg > 1             ? xfft_forward_kernel<NN, T, true, WIDE>
+              : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne>
+              : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin>
+                              : xfft_forward_kernel<NN, T, false, WIDE, kSegFull>;
+  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
+                     static_cast<const T2*>(tw.buf));
+}
+
+// ---- z-direction physical stage -------------------------------------------------------------
+__device__ __forceinline__ void atomic_max_pos(float* p, float v) {
+  atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}
+
+// One wave per (y,x) row up to 1024 points; a block holds ZWT rows and each wave owns one LDS row
+// buffer, so there is no block barrier between the gather, the five FFTs, the product and the
+// extraction.  The six physical fields stay in registers (thread t of a row owns points
+// n = t + TPR i).  2048-point rows take two waves (TPR = 128) with block barriers between the
+// passes: at one wave per row the 6 x 32 points per lane needed ~430 registers (one wave per
+// SIMD; 180 spilled VGPRs in fp64), at two waves the register budget of the 1024-point kernel.
+// Below 1024 points a wave holds several rows (TPR < 64 threads per row): every thread keeps 16
+// (fp32) or 8 (fp64) points per field, and the wave's transforms cover all its rows at once, so a
+// 128-point row no longer leaves 56 of 64 lanes idle in its first radix-16 pass.
+constexpr int ZW = 4;
+// threads per row: 16 (fp32) / 8 (fp64) points per thread, rounded up to a power of two so a
+// wave holds a whole number of rows (lengths 3*2^k, 5*2^k: 12 / 10 points per thread)
+template <int NZP>
+constexpr int zphys_tpr(int esz = 4) {
+  return esz == 4 ? (NZP >= 16 ? pow2_ceil((NZP + 15) / 16) : 1)
+                  : (NZP >= 1024 ? 128 : (NZP >= 16 ? pow2_ceil((NZP + 7) / 8) : 1));
+}
+// rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32);
+// 4 waves' worth of rows below 64 threads per row
+template <int NZP, typename T, int TPR = zphys_tpr<NZP>(sizeof(T))>
+constexpr int zphys_rows() {
+  return TPR < 64 ? ZW * 64 / TPR : (NZP >= 2048 || (sizeof(T) == 4 && TPR == 128) ? 2 : ZW);
+}
+
+template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
+          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 1>
+__global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+                                                         const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  constexpr int PITCH = FftPitch<NZP>::value;
+  constexpr int TPR = TPRT;  // threads per row
+  constexpr int NWB = ZWT * TPR / 64;     // waves per block
+  constexpr int TPRF = TPR < 64 ? 64 : TPR;  // threads per transform call (one wave or a row)
+  constexpr int RWW = TPR < 64 ? 64 / TPR : 1;  // rows per transform call
+  constexpr int EP = (NZP + TPR - 1) / TPR;  // points per thread
+  __shared__ T2 s[ZWT * PITCH];
+  constexpr int TS = FftPlan<NZP>::TSIZE;
+  // real H_z: half-length complex transform + post twiddles (HalfPlan) where one exists
+  using Hp = HalfPlan<NZP>;
+  constexpr bool kHalf = ZH && Hp::ok;
+  constexpr int TSA = TS + (kHalf ? Hp::SIZE : 0);
+  __shared__ T2 tws[TSA];  // twiddles staged once per block: LDS latency instead of L2 in the passes
+  __shared__ float red[4][NWB];
+  // lane: wave lane (reductions); t: thread within the row; w: row within the block
+  const int tid = threadIdx.x, lane = tid & 63, t = tid % TPR, w = tid / TPR;
+  for (int i = tid; i < TSA; i += ZWT * TPR) tws[i] = tw[i];
+  __syncthreads();
+  T2* row = s + w * PITCH;
+  T2* frow = s + (tid / TPRF) * RWW * PITCH;  // first row of this thread's transform group
+  const int ft = tid % TPRF;
+  const long long nrows = static_cast<long long>(a.ny) * a.NX;
+  const long long r = static_cast<long long>(blockIdx.x) * ZWT + w;
+  const int Kz = a.nkz - 1, nkz = a.nkz;
+  const long long fs = a.field_stride;
+  float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
+  // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz)
+  auto zaddr = [&](int k) -> long long {
+    if constexpr (SEG) {
+      const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
+      return sp.off + r * sp.count + (k - sp.start);
+    } else {
+      return r * nkz + k;
+    }
+  };
+
+  // (a persistent variant looping over row groups made the compiler hold ~380 registers: one wave
+  // per SIMD, 49.8 vs 44.3 ms/step).  Rows past the end (TPR < 64 only: the host checks
+  // nrows % ZWT == 0 otherwise) run the transforms on zeros and skip every global access.
+  const bool rv = r < nrows;
+  {
+    T2 ph[3][EP];
+    constexpr int MK = (NZP / 2 + TPR - 1) / TPR;
+    auto fetch = [&](int p, T2 (&va)[MK], T2 (&vb)[MK]) {
+      const T2* A = fields + (2 * p) * fs;
+      const T2* B = fields + (2 * p + 1) * fs;
+#pragma unroll
+      for (int i = 0; i < MK; ++i) {
+        const int k = t + TPR * i;
+        const bool ld = k < nkz && rv;
+        const long long o = ld ? zaddr(k) : 0;
+        va[i] = ld ? A[o] : T2{0, 0};
+        vb[i] = ld ? B[o] : T2{0, 0};
+      }
+    };
+    // the next pair's loads are in flight during each transform where the 24 registers fit (fp32,
+    // <= 1024 points, one segment); elsewhere each pair is loaded right before its transform
+    constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
+    T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
+    if constexpr (kPrefetch) fetch(0, pa, pb);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      T2 va[MK], vb[MK];
+      if constexpr (kPrefetch) {
+#pragma unroll
+        for (int i = 0; i < MK; ++i) {
+          va[i] = pa[i];
+          vb[i] = pb[i];
+        }
+      } else {
+        const T2* A = fields + (2 * p) * fs;
+        const T2* B = fields + (2 * p + 1) * fs;
+#pragma unroll
+        for (int i = 0; i < MK; ++i) {
+          const int k = t + TPR * i;
+          const bool ld = k < nkz && rv;
+          const long long o = ld ? zaddr(k) : 0;
+          va[i] = ld ? A[o] : T2{0, 0};
+          vb[i] = ld ? B[o] : T2{0, 0};
+        }
+      }
+      // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
+      // (a real z-row has a real mean), zero padding between Kz and N-Kz.
+#pragma unroll
+      for (int i = 0; i < MK; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz) {
+          if (k == 0) {
+            row[fft_pidx(0)] = T2{va[i].x, vb[i].x};
+          } else {
+            row[fft_pidx(k)] = T2{va[i].x - vb[i].y, va[i].y + vb[i].x};
+            row[fft_pidx(NZP - k)] = T2{va[i].x + vb[i].y, vb[i].x - va[i].y};
+          }
+        }
+      }
+      for (int k = Kz + 1 + t; k < NZP - Kz; k += TPR) row[fft_pidx(k)] = T2{0, 0};
+      if constexpr (kPrefetch) {
+        if (p < 2) fetch(p + 1, pa, pb);
+      }
+      row_sync<TPRF>();
+      if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, true, TPRF>(frow, tws, ft);
+#pragma unroll
+      for (int i = 0; i < EP; ++i) {
+        const int n = t + TPR * i;
+        ph[p][i] = n < NZP ? row[fft_pidx(n)] : T2{0, 0};
+      }
+      row_sync<TPRF>();
+    }
+    // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
+    const int yl = rv ? static_cast<int>(r / a.NX) : 0;
+    const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    T hz[EP];
+#pragma unroll
+    for (int i = 0; i < EP; ++i) {
+      const T u = ph[0][i].x, v = ph[0][i].y, ww = ph[1][i].x, wx = ph[1][i].y, wy = ph[2][i].x, wz = ph[2][i].y;
+      const T hx = v * wz - ww * wy, hy = ww * wx - u * wz;
+      hz[i] = u * wy - v * wx;
+      const float au = fabsf(static_cast<float>(u)), av = fabsf(static_cast<float>(v)), aw = fabsf(static_cast<float>(ww));
+      mu = fmaxf(mu, au);
+      mv = fmaxf(mv, av);
+      mw = fmaxf(mw, aw);
+      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+      const int n = t + TPR * i;
+      if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
+    }
+    row_sync<TPRF>();
+    const T sc = static_cast<T>(0.5 * a.scale);
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
+    // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
+    // (unrolled: all LDS reads are issued before the global stores)
+    constexpr int MKO = (NZP / 2 + TPR - 1) / TPR;
+    {
+      T2 z0[MKO], z1[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx(k == 0 ? 0 : NZP - k)];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz && rv) {
+          const T2 Z = z0[i], Zm = z1[i];
+          const long long o = zaddr(k);
+          fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+          fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+        }
+      }
+    }
+    row_sync<TPRF>();
+    if constexpr (kHalf) {
+      // H_z is real: z_m = Hz_2m + i Hz_2m+1 (scalar LDS stores, conflict-free), an N/2-point
+      // transform, then Hz_k = E_k + W_N^k O_k (one N-point complex transform per row saved)
+      T* rowf = reinterpret_cast<T*>(row);
+#pragma unroll
+      for (int i = 0; i < EP; ++i) {
+        const int n = t + TPR * i;
+        if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
+      }
+      row_sync<TPRF>();
+      const T2* htw = tws + TS;
+      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPRF>(row, htw, ft);
+      T2 z0[MKO], z1[MKO], wk[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx((Hp::H - k) & (Hp::H - 1))];
+          wk[i] = htw[k];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz && rv) {
+          // 2E = Z_k + conj Z_{H-k}; 2O = (Z_k - conj Z_{H-k}) / i
+          const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
+          const T2 O2{z0[i].y + z1[i].y, z1[i].x - z0[i].x};
+          const T2 X = cadd(E2, cmul_tw<false>(O2, wk[i]));
+          fields[2 * fs + zaddr(k)] = T2{X.x * sc, X.y * sc};
+        }
+      }
+    } else {
+#pragma unroll
+    for (int i = 0; i < EP; ++i) {
+      const int n = t + TPR * i;
+      if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
+    }
+    row_sync<TPRF>();
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
+    {
+      T2 z0[MKO], z1[MKO];
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz) {
+          z0[i] = row[fft_pidx(k)];
+          z1[i] = row[fft_pidx(k == 0 ? 0 : NZP - k)];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz && rv) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
+      }
+    }
+    }
+  }
+  // block maxima -> one atomicMax per block and quantity
+  for (int o = 32; o >= 1; o >>= 1) {
+    mu = fmaxf(mu, __shfl_xor(mu, o));
+    mv = fmaxf(mv, __shfl_xor(mv, o));
+    mw = fmaxf(mw, __shfl_xor(mw, o));
+    mc = fmaxf(mc, __shfl_xor(mc, o));
+  }
+  if (lane == 0) {
+    red[0][tid >> 6] = mu;
+    red[1][tid >> 6] = mv;
+    red[2][tid >> 6] = mw;
+    red[3][tid >> 6] = mc;
+  }
+  __syncthreads();
+  if (tid < 4 && a.maxima) {
+    float m = 0.f;
+    for (int i = 0; i < NWB; ++i) m = fmaxf(m, red[tid][i]);
+    atomic_max_pos(&a.maxima[tid], m);
+  }
+}
+
+// ---- register-resident z stage (NZP = 64 M, M = 16: the 1024-point rows of the headline grid) --
+// The LDS-pass FFT above makes 4 LDS round trips per transform (gather, 3 Stockham passes) and is
+// latency-bound at 2 waves/SIMD.  Here each transform is a four-step FFT N = M x 64 held in the
+// wave's registers: lane k2 owns Z[k2 + 64 k1] (loaded straight from global memory, conjugate
+// mirror included), an M-point DFT in registers, a twiddle, ONE LDS transpose, a 16-point DFT in
+// registers, a twiddle and a 4-point DFT across the lanes of a quad (DPP quad_perm, no LDS).  The
+// physical row stays in registers in the permuted order n = n1 + M (c + 16 br(a)), which is exactly
+// the input order of the reverse network used for the forward transforms of H.
+constexpr int kQuadXor1 = 0xB1;  // DPP quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;  // DPP quad_perm [2,3,0,1]
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+template <int CTRL, typename T2>
+__device__ __forceinline__ T2 quad_swap(T2 v) {
+  return T2{dpp_mov<CTRL>(v.x), dpp_mov<CTRL>(v.y)};
+}
+// one radix-2 stage across a lane pair: low lane a + b, high lane a - b (b = partner's value)
+template <int CTRL, typename T2>
+__device__ __forceinline__ T2 quad_bfly(T2 v, bool high) {
+  using T = decltype(v.x);
+  const T2 p = quad_swap<CTRL>(v);
+  const T s = high ? T(-1) : T(1);
+  return T2{p.x + s * v.x, p.y + s * v.y};
+}
+// natural order in (lane a of the quad holds y_a) -> lane a holds Y[br(a)] (br swaps 1 and 2)
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 quad_dft4_nat_in(T2 v, int a) {
+  v = quad_bfly<kQuadXor2>(v, (a & 2) != 0);
+  if (a == 3) v = mul_mi<INV>(v);
+  return quad_bfly<kQuadXor1>(v, (a & 1) != 0);
+}
+// bit-reversed order in (lane a holds y_br(a)) -> natural order out (lane a holds Y[a])
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 quad_dft4_br_in(T2 v, int a) {
+  v = quad_bfly<kQuadXor1>(v, (a & 1) != 0);
+  if (a == 3) v = mul_mi<INV>(v);
+  return quad_bfly<kQuadXor2>(v, (a & 2) != 0);
+}
+template <typename T2>
+__device__ __forceinline__ T2 cmulc(T2 a, T2 w) {  // a * conj(w)
+  return T2{a.x * w.x + a.y * w.y, a.y * w.x - a.x * w.y};
+}
+
+constexpr int kRegPitch = 68;  // transpose row pitch (64 + 4): conflict-free b64 column reads
+
+// Inverse transform of one spectral row held as z[k1] = Z[lane + 64 k1] (unnormalised, +i sign);
+// on return z[c] = x[n1 + M (c + 16 br(a))], lane = 4 g + a, n1 = g (M = 16).
+// buf: this wave's M x kRegPitch transpose buffer; tw1: [M][64] W_N^(n1 k2); tw64: [4][16] W_64^(a c).
+template <int M, typename T2>
+__device__ __forceinline__ void reg_fft_inv(T2 (&z)[M], T2* buf, const T2* tw1, const T2* tw64, int lane) {
+  static_assert(M == 16, "register z-stage FFT: M = 16 (N = 1024)");
+  dft16<true>(z);  // over k1 -> n1
+#pragma unroll
+  for (int n1 = 1; n1 < M; ++n1) z[n1] = cmulc(z[n1], tw1[n1 * 64 + lane]);
+#pragma unroll
+  for (int n1 = 0; n1 < M; ++n1) buf[n1 * kRegPitch + lane] = z[n1];
+  __builtin_amdgcn_wave_barrier();
+  const int g = lane >> 2, a = lane & 3;
+#pragma unroll
+  for (int b = 0; b < 16; ++b) z[b] = buf[g * kRegPitch + a + 4 * b];
+  __builtin_amdgcn_wave_barrier();
+  dft16<true>(z);  // over b -> c
+#pragma unroll
+  for (int c = 1; c < 16; ++c)
+    if (a != 0) z[c] = cmulc(z[c], tw64[a * 16 + c]);
+#pragma unroll
+  for (int c = 0; c < 16; ++c) z[c] = quad_dft4_nat_in<true>(z[c], a);
+}
+
+// Forward transform of a physical row in the register order produced by reg_fft_inv; on return
+// z[k1] = Z[lane + 64 k1] (unnormalised, -i sign).
+template <int M, typename T2>
+__device__ __forceinline__ void reg_fft_fwd(T2 (&z)[M], T2* buf, const T2* tw1, const T2* tw64, int lane) {
+  static_assert(M == 16, "register z-stage FFT: M = 16 (N = 1024)");
+  const int g = lane >> 2, a = lane & 3;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) z[c] = quad_dft4_br_in<false>(z[c], a);  // over d -> e = a
+#pragma unroll
+  for (int c = 1; c < 16; ++c)
+    if (a != 0) z[c] = cmul(z[c], tw64[a * 16 + c]);
+  dft16<false>(z);  // over c -> f
+#pragma unroll
+  for (int f = 0; f < 16; ++f) buf[g * kRegPitch + a + 4 * f] = z[f];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int n1 = 0; n1 < M; ++n1) z[n1] = buf[n1 * kRegPitch + lane];
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int n1 = 1; n1 < M; ++n1) z[n1] = cmul(z[n1], tw1[n1 * 64 + lane]);
+  dft16<false>(z);  // over n1 -> k1
+}
+
+template <int M, typename T, bool SEG>
+__global__ void __launch_bounds__(256) zphys_reg_kernel(ZArgs a, typename C2<T>::type* fields,
+                                                        const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  constexpr int NZP = 64 * M;
+  __shared__ T2 tbuf[ZW][M * kRegPitch];
+  __shared__ T2 tws[NZP + 64];  // [M][64] W_N^(n1 k2), then [4][16] W_64^(a c)
+  __shared__ float red[4][ZW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < NZP + 64; i += ZW * 64) tws[i] = tw[i];
+  __syncthreads();
+  const T2* tw1 = tws;
+  const T2* tw64 = tws + NZP;
+  T2* buf = tbuf[w];
+  const long long nrows = static_cast<long long>(a.ny) * a.NX;
+  const long long r = static_cast<long long>(blockIdx.x) * ZW + w;
+  const int nkz = a.nkz;
+  const long long fs = a.field_stride;
+  float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
+  auto zaddr = [&](int k) -> long long {
+    if constexpr (SEG) {
+      const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
+      return sp.off + r * sp.count + (k - sp.start);
+    } else {
+      return r * nkz + k;
+    }
+  };
+
+  if (r < nrows) {  // wave-uniform
+    T2 ph[3][M];
+    // Only the retained half is loaded (slot i = mode lane + 64 i, i < M/2); the conjugate mirror
+    // Z_{N-k} comes from lane 64 - lane (slot M-1-k1; lane 0: its own slot M-k1) by a lane
+    // permute.  The loads of field pair p+1 are issued before the transform of pair p.
+    constexpr int MH = M / 2;
+    T2 la[2][MH], lb[2][MH];
+    auto load_pair = [&](int p, T2 (&va)[MH], T2 (&vb)[MH]) {
+      const T2* A = fields + (2 * p) * fs;
+      const T2* B = fields + (2 * p + 1) * fs;
+#pragma unroll
+      for (int i = 0; i < MH; ++i) {
+        const int k = lane + 64 * i;
+        const bool ok = k < nkz;
+        const long long o = ok ? zaddr(k) : 0;
+        va[i] = ok ? A[o] : T2{0, 0};
+        vb[i] = ok ? B[o] : T2{0, 0};
+      }
+    };
+    load_pair(0, la[0], lb[0]);
+    const int src = (64 - lane) & 63;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int cur = p & 1;
+      if (p < 2) load_pair(p + 1, la[cur ^ 1], lb[cur ^ 1]);
+      // Z_k = A_k + i B_k (k < nkz), Z_{N-k} = conj(A_k) + i conj(B_k); kz = 0 imaginary parts dropped
+#pragma unroll
+      for (int k1 = 0; k1 < MH; ++k1) {
+        const T2 A = la[cur][k1], B = lb[cur][k1];
+        ph[p][k1] = (lane == 0 && k1 == 0) ? T2{A.x, B.x} : T2{A.x - B.y, A.y + B.x};
+      }
+#pragma unroll
+      for (int k1 = MH; k1 < M; ++k1) {
+        T2 A{__shfl(la[cur][M - 1 - k1].x, src), __shfl(la[cur][M - 1 - k1].y, src)};
+        T2 B{__shfl(lb[cur][M - 1 - k1].x, src), __shfl(lb[cur][M - 1 - k1].y, src)};
+        if (lane == 0) {  // N - k = 64 (M - k1): own slot M - k1 (k1 = M/2 is the Nyquist mode: zero)
+          A = k1 > MH ? la[cur][(M - k1) % MH] : T2{0, 0};
+          B = k1 > MH ? lb[cur][(M - k1) % MH] : T2{0, 0};
+        }
+        ph[p][k1] = T2{A.x + B.y, B.x - A.y};
+      }
+      if (!(a.diag & 1)) reg_fft_inv<M>(ph[p], buf, tw1, tw64, lane);
+    }
+    // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
+    const int yl = static_cast<int>(r / a.NX);
+    const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    T2 hxy[M], hz[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const T u = ph[0][i].x, v = ph[0][i].y, ww = ph[1][i].x, wx = ph[1][i].y, wy = ph[2][i].x, wz = ph[2][i].y;
+      hxy[i] = T2{v * wz - ww * wy, ww * wx - u * wz};
+      hz[i] = T2{u * wy - v * wx, T(0)};
+      const float au = fabsf(static_cast<float>(u)), av = fabsf(static_cast<float>(v)), aw = fabsf(static_cast<float>(ww));
+      mu = fmaxf(mu, au);
+      mv = fmaxf(mv, av);
+      mw = fmaxf(mw, aw);
+      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+    }
+    if (!(a.diag & 1)) {
+      reg_fft_fwd<M>(hxy, buf, tw1, tw64, lane);
+      reg_fft_fwd<M>(hz, buf, tw1, tw64, lane);
+    }
+    // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i); Z_{N-k}
+    // lives in lane 64 - lane at k1' = M-1-k1 (lane 0: its own k1' = M - k1)
+    const T sc = static_cast<T>(0.5 * a.scale), sz = static_cast<T>(a.scale);
+    constexpr int MKO = (NZP / 2 + 63) / 64;
+#pragma unroll
+    for (int k1 = 0; k1 < MKO; ++k1) {
+      const int k = lane + 64 * k1;
+      const int src = (64 - lane) & 63;
+      T2 zm{__shfl(hxy[M - 1 - k1].x, src), __shfl(hxy[M - 1 - k1].y, src)};
+      if (lane == 0) zm = hxy[(M - k1) % M];
+      if (k < nkz) {
+        const T2 Z = hxy[k1];
+        const long long o = zaddr(k);
+        fields[0 * fs + o] = T2{(Z.x + zm.x) * sc, (Z.y - zm.y) * sc};
+        fields[1 * fs + o] = T2{(Z.y + zm.y) * sc, -(Z.x - zm.x) * sc};
+        fields[2 * fs + o] = T2{hz[k1].x * sz, hz[k1].y * sz};
+      }
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    mu = fmaxf(mu, __shfl_xor(mu, o));
+    mv = fmaxf(mv, __shfl_xor(mv, o));
+    mw = fmaxf(mw, __shfl_xor(mw, o));
+    mc = fmaxf(mc, __shfl_xor(mc, o));
+  }
+  if (lane == 0) {
+    red[0][w] = mu;
+    red[1][w] = mv;
+    red[2][w] = mw;
+    red[3][w] = mc;
+  }
+  __syncthreads();
+  if (tid < 4 && a.maxima) {
+    float m = 0.f;
+    for (int i = 0; i < ZW; ++i) m = fmaxf(m, red[tid][i]);
+    atomic_max_pos(&a.maxima[tid], m);
+  }
+}
+
+// CHANNEL_ZREG=1 selects the register-resident z stage at Nzp = 1024.  Measured at 1024x385x1024
+// fp32 (r2p): 3.5x fewer LDS instructions than the LDS-pass kernel but +17 % VALU and +65 %
+// wave-parked cycles (one transpose wait + per-FFT twiddle reads per transform at 2 waves/SIMD):
+// 51.2 vs 50.0 ms/step, so the LDS-pass kernel stays the default.
+inline bool zreg_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_ZREG");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+// CHANNEL_ZHALF=0: H_z through a full-length complex transform (A/B of the half-length path)
+inline bool zhalf_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_ZHALF");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <int NN, typename T, int TPR, int WPE = 1>
+static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s, bool zh) {
+  using T2 = typename C2<T>::type;
+  constexpr int ZR = zphys_rows<NN, T, TPR>();
+  const long long nrows = static_cast<long long>(a.ny) * a.NX;
+  auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
+                         : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
+  dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
+  CH_CHECK(TPR < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
+  hipLaunchKernelGGL(kern, grid, dim3(ZR * TPR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
+}
+
+// CHANNEL_ZTPR=64|128: threads per 1024-point fp32 row (A/B; see zphys_tpr for the default).  Two
+// waves per row take 152 instead of 218 VGPRs (3 waves/SIMD) but pay a block barrier per pass:
+// measured 48.8 vs 46.3 ms/step on the headline grid, so one wave per row stays the default.
+// CHANNEL_ZWPE=3: the one-wave-per-row 1024-point fp32 kernel compiled for 3 waves per SIMD (168
+// VGPRs, ~20 spilled) instead of 2 (216 VGPRs, no spills) (A/B).  Measured on the headline grid,
+// same box, alternating: 47.4 vs 45.5 ms/step, so 2 waves per SIMD without spills stays the default
+inline int zwpe_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_ZWPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+inline int ztpr_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_ZTPR");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+// ---- standalone batched C2C (tests) ----------------------------------------------------------
+template <int N, typename T, bool INV>
+__global__ void __launch_bounds__(256) fft_test_kernel(typename C2<T>::type* data, int batch,
+                                                       const typename C2<T>::type* tw) {
+  using T2 = typename C2<T>::type;
+  constexpr int PITCH = FftPitch<N>::value;
+  __shared__ T2 s[4 * PITCH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long rw = static_cast<long long>(blockIdx.x) * 4 + w;
+  if (rw >= batch) return;  // wave-uniform; no block barriers below
+  T2* row = s + w * PITCH;
+  for (int x = lane; x < N; x += 64) row[fft_pidx(x)] = data[rw * N + x];
+  __builtin_amdgcn_wave_barrier();
+  wave_fft<N, 1, PITCH, INV>(row, tw, lane);
+  for (int x = lane; x < N; x += 64) data[rw * N + x] = row[fft_pidx(x)];
+}
+
+// ---- per-length entry points (instantiated by the length-family translation units) ----------
+template <int NN>
+void fft_xb_len(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s) {
+  if (fp64) {
+    xb_launch_cfg<NN, double, 0>(a, src, phys, tw, s);
+  } else if constexpr (NN == 512 || NN == 1024) {
+    if (xwide_enabled()) xb_launch_cfg<NN, float, 1>(a, src, phys, tw, s);
+    else xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
+  } else {
+    xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
+  }
+}
+template <int NN>
+void fft_xf_len(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s) {
+  if (fp64) {
+    xf_launch_cfg<NN, double, 0>(a, phys, dst, tw, s);
+  } else if constexpr (NN == 512 || NN == 1024) {
+    if (xwide_enabled()) xf_launch_cfg<NN, float, 1>(a, phys, dst, tw, s);
+    else xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);
+  } else {
+    xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);
+  }
+}
+template <int NN, typename T>
+void fft_zp_len_t(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s) {
+  const bool zh = zhalf_enabled();
+  constexpr int DEF = zphys_tpr<NN>(sizeof(T));
+  if constexpr (sizeof(T) == 4 && NN == 1024) {
+    constexpr int ALT = DEF == 64 ? 128 : 64;
+    if (ztpr_env() == ALT) zphys_launch_tpr<NN, T, ALT>(a, fields, tw, s, zh);
+    else if (DEF == 64 && zwpe_env() == 3) zphys_launch_tpr<NN, T, DEF, 3>(a, fields, tw, s, zh);
+    else zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
+  } else {
+    zphys_launch_tpr<NN, T, DEF>(a, fields, tw, s, zh);
+  }
+}
+template <int NN>
+void fft_zp_len(const ZArgs& a, void* fields, const Twiddles& tw, bool fp64, hipStream_t s) {
+  if (fp64) fft_zp_len_t<NN, double>(a, fields, tw, s);
+  else fft_zp_len_t<NN, float>(a, fields, tw, s);
+}
+template <int NN>
+void fft_test_len(void* data, int batch, int dir, const Twiddles& tw, bool fp64, hipStream_t s) {
+  dim3 grid((batch + 3) / 4);
+  if (fp64) {
+    if (dir > 0) hipLaunchKernelGGL((fft_test_kernel<NN, double, true>), grid, dim3(256), 0, s, static_cast<double2*>(data), batch, static_cast<const double2*>(tw.buf));
+    else hipLaunchKernelGGL((fft_test_kernel<NN, double, false>), grid, dim3(256), 0, s, static_cast<double2*>(data), batch, static_cast<const double2*>(tw.buf));
+  } else {
+    if (dir > 0) hipLaunchKernelGGL((fft_test_kernel<NN, float, true>), grid, dim3(256), 0, s, static_cast<float2*>(data), batch, static_cast<const float2*>(tw.buf));
+    else hipLaunchKernelGGL((fft_test_kernel<NN, float, false>), grid, dim3(256), 0, s, static_cast<float2*>(data), batch, static_cast<const float2*>(tw.buf));
+  }
+}
+
+// the lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280)
+#define CH_FFT_POW2_LENGTHS(X) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048)
+#define CH_FFT_R3_LENGTHS(X) X(48) X(96) X(192) X(384) X(768) X(1536)
+#define CH_FFT_R5_LENGTHS(X) X(80) X(160) X(320) X(640) X(1280)
+#define CH_FFT_INSTANTIATE(NN)                                                                              \
+  template void fft_xb_len<NN>(const XArgs&, const XSrc&, void*, const Twiddles&, bool, hipStream_t);      \
+  template void fft_xf_len<NN>(const XArgs&, const void*, const XDst&, const Twiddles&, bool, hipStream_t); \
+  template void fft_zp_len<NN>(const ZArgs&, void*, const Twiddles&, bool, hipStream_t);                    \
+  template void fft_test_len<NN>(void*, int, int, const Twiddles&, bool, hipStream_t);
+// (extern declarations per entry point: an extern template covers one declaration)
+#define CH_FFT_EXTERN_ALL(NN)                                                                                   \
+  extern template void fft_xb_len<NN>(const XArgs&, const XSrc&, void*, const Twiddles&, bool, hipStream_t);      \
+  extern template void fft_xf_len<NN>(const XArgs&, const void*, const XDst&, const Twiddles&, bool, hipStream_t); \
+  extern template void fft_zp_len<NN>(const ZArgs&, void*, const Twiddles&, bool, hipStream_t);                    \
+  extern template void fft_test_len<NN>(void*, int, int, const Twiddles&, bool, hipStream_t);
+CH_FFT_POW2_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R3_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R5_LENGTHS(CH_FFT_EXTERN_ALL)
+
+}  // namespace channel

@@ -1,0 +1,787 @@
+// K-SPEC: the fused spectral (y-line) substep kernel.
+//
+// Per (kx,kz) line it does everything the reference does in y between two FFT rounds
+// (SURVEY §7.3 K-SPEC-A/B):
+//   calcHvg/calcHvv (nonLinear_kernels.cu:94-190), rk_step_1/2 (RK3_kernels.cu:6-153),
+//   implicitSolver_double x2 (implicitStep_nu_double.cu:227-247), bilaplaSolver_double
+//   (bilplacSolver_double.cu:320-348: implicit phi, Helmholtz v, D1 v, influence matrix),
+//   meanURKstep_1/2 + forcing (meanUevol.c:201-221, 439-567, on the device for line (0,0)),
+//   calcUW (nonLinear_kernels.cu:8-92), the wz/wx D1 calls and calcOmega
+//   (convolution.c:7-20, convolution_kernels.cu:7-66), calcSt plane sums (statistics.cu:7-95).
+// The reference runs these as ~50 launches + 44 cusparse calls + 8 D2D copies per substep with
+// float<->double casts through HBM.  Here one launch reads 7 fields and writes 10, all y-work is
+// fp64 in registers, and the wall-normal operators are applied in "M-form" (the compact D2 mass
+// matrix multiplies the equation), so the explicit viscous term needs no solve at all.
+//
+// Layout: one wave per line (lane l holds rows l*R .. l*R+R-1), W lines per workgroup, one
+// persistent workgroup per CU walking tiles of W lines.  Per CU the LDS holds the coefficient
+// tables (staged once), two staging tiles [r][lane][line] (pitch W+1: conflict-free column
+// reads; global side: W consecutive complex values per y row) and one cross-lane scratch line per
+// wave for the PCR strides >= 4 (yline_device.hpp, kXlLds).  The register budget is laid out for
+// 2 waves per SIMD at 8 lines (fp32, R <= 8): the solves work in place (SPIKE form), the constant
+// D1 factorisation is read from LDS where it is used, and only NS input fields are prefetched into
+// registers (distance NS in the input sequence; the next tile's first inputs are issued before the
+// last solve of the current one).
+// This header holds the kernel template; kspec.hip (PAR = 0) and kspec_par*.hip (the parity
+// variants) instantiate it in separate translation units so they compile in parallel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "channel/common.hpp"
+#include "channel/fft_device.hpp"
+#include "channel/kernels.hpp"
+#include "channel/kspec_config.hpp"
+#include "channel/yline_device.hpp"
+
+namespace channel {
+
+using namespace dev;
+
+// ------------------------------------------------------------------------------------------
+// Staging of W lines through an LDS tile (double-buffered where tile2 is set) with NS register
+// prefetch slots (or address-only slots where registers are short: R > 8).
+// Tile layout: y-major, row y at y*PITCH + (y/R)*G (W lines + 1 pad slot per row).  A wave's
+// column read (rows lane*R + r) then strides R*PITCH + G slots between lanes, an odd number of
+// 8-B words, which spreads the 32 lanes of each ds_read_b64 half over all 64 banks; G = 1 fixes
+// the parity for even R.  Thread t of the cooperative copies handles rows t/W + 64 q of line t%W,
+// so both the LDS and the global addresses are one base plus compile-time / scalar offsets.
+template <int R, typename T, int W, int NS>
+struct Stage {
+  using T2 = typename Cplx<T>::type;
+  static constexpr int PITCH = W + 1;
+  static constexpr int G = (R * PITCH) % 2 == 1 ? 0 : 1;
+  static constexpr int TILE = 64 * R * PITCH + (G ? 64 : 0);
+  static constexpr int RPB = 64;  // rows per copy pass: W * 64 threads / W lines
+  static constexpr bool kRegSlots = R <= 8;
+  T2* tile;   // buffer of the last staging (column() reads it)
+  T2* tile2;  // the other buffer (nullptr: single-buffered)
+  int N, lines, line0, w, lane;
+  // Per-thread element offset of (row y0 = tid / W, line line0 + tid % W) and of one 64-row pass:
+  // re-derived per tile through an opaque copy, so the per-field addresses are formed at their
+  // use (a 64-bit field base + a 32-bit offset: global_load/store saddr forms) instead of being
+  // hoisted out of the tile loop into ~2 registers per field
+  unsigned toff = 0, pstride = 0;
+  T2 pend[kRegSlots ? NS : 1][R];
+  const T2* dsrc[kRegSlots ? 1 : NS];
+  unsigned doff[kRegSlots ? 1 : NS];
+
+  static __device__ __forceinline__ int row_off(int y) { return y * PITCH + (G ? (y / R) : 0); }
+  __device__ __forceinline__ unsigned thread_off(int l0) const {
+    const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+    unsigned o = static_cast<unsigned>(y0) * static_cast<unsigned>(lines) + static_cast<unsigned>(min(l0 + l, lines - 1));
+    asm volatile("" : "+v"(o));
+    return o;
+  }
+  __device__ __forceinline__ void set_line0(int l0) {
+    line0 = l0;
+    toff = thread_off(l0);
+  }
+  __device__ __forceinline__ void next_tile() {
+    if (tile2) {
+      T2* t = tile2;
+      tile2 = tile;
+      tile = t;
+    } else {
+      lds_barrier();  // single buffer: the previous staging's reads must be done
+    }
+  }
+  // Issue the global loads of a field (rows y0 + 64 q, q < R, of this thread's line) without
+  // waiting.  Unconditional loads (a guarded load becomes a branch and a vmcnt(0) wait per
+  // element): rows >= N read row N-1 (never committed), lines >= lines read the last line (staged
+  // but never stored).
+  template <int S>
+  __device__ __forceinline__ void prefetch_at(const T2* __restrict__ src, int l0) {
+    const unsigned o = thread_off(l0);
+    if constexpr (!kRegSlots) {
+      dsrc[S] = src;
+      doff[S] = o;
+    } else {
+      const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+      // rows >= N read row N-1 of the same (clamped) line
+      const unsigned last = static_cast<unsigned>(N - 1) * static_cast<unsigned>(lines) +
+                            static_cast<unsigned>(min(l0 + l, lines - 1));
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const unsigned oq = y0 + RPB * q < N ? o + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines) : last;
+        pend[S][q] = src[oq];
+      }
+    }
+  }
+  // Stage the prefetched field through the LDS tile and return this wave's line.  Rows >= N of
+  // both tiles are zero from the start and never written (the solves keep padding rows at exactly
+  // zero), so the column read needs no masks.
+  template <int S>
+  __device__ __forceinline__ void commit(double (&x)[2][R]) {
+    next_tile();
+    const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int y = y0 + RPB * q;
+      if (y < N) {
+        if constexpr (kRegSlots) {
+          tile[row_off(y) + l] = pend[S][q];
+        } else {
+          tile[row_off(y) + l] = dsrc[S][doff[S] + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines)];
+        }
+      }
+    }
+    lds_barrier();
+    column(x);
+  }
+  // This wave's line as it sits in the tile.  After store() the tile still holds the stored
+  // field, so a value just written out can be re-read from LDS (at storage precision) without
+  // a global round trip, as long as no staging has happened since.
+  __device__ __forceinline__ void column(double (&x)[2][R]) const {
+    const T2* c = tile + row_off(lane * R) + w;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const T2 v = c[r * PITCH];
+      x[0][r] = static_cast<double>(v.x);
+      x[1][r] = static_cast<double>(v.y);
+    }
+  }
+  __device__ __forceinline__ void load(const T2* __restrict__ src, double (&x)[2][R]) {
+    prefetch_at<0>(src, line0);
+    commit<0>(x);
+  }
+  // rows >= N are written too: the operators keep them at exactly zero
+  __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&x)[2][R]) { store(dst, x[0], x[1]); }
+  // (re, im) rows of a line, optionally scaled (wave-uniform)
+  __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&re)[R], const double (&im)[R],
+                                        double sc = 1.0) {
+    next_tile();
+    {
+      T2* c = tile + row_off(lane * R) + w;
+#pragma unroll
+      for (int r = 0; r < R; ++r) c[r * PITCH] = T2{static_cast<T>(sc * re[r]), static_cast<T>(sc * im[r])};
+    }
+    lds_barrier();
+    const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+    if (line0 + l < lines) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int y = y0 + RPB * q;
+        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines)] = tile[row_off(y) + l];
+      }
+    }
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void czero(double (&x)[2][R]) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[k][r] = 0.0;
+}
+
+// overflow-safe cosh(l y)/cosh(l) and sinh(l y)/sinh(l) (and their y-derivatives), |y| <= 1, l > 0
+__device__ __forceinline__ void chs_profiles(double l, double y, double& C, double& S, double& dC, double& dS) {
+  const double ep = exp(l * (y - 1.0)), em = exp(-l * (y + 1.0)), e2 = exp(-2.0 * l);
+  C = (ep + em) / (1.0 + e2);
+  S = (ep - em) / (1.0 - e2);
+  dC = l * (ep - em) / (1.0 + e2);
+  dS = l * (ep + em) / (1.0 - e2);
+}
+
+// per-wave exchange scratch (kXlLds)
+template <int R, int W>
+constexpr int kspec_scratch_doubles() {
+  return kspec_xmode<R, float>() == kXlLds ? W * xl_scratch_doubles(kKspecXK) : 1;
+}
+template <int R, typename T, int W>
+constexpr int kspec_lds_tables_doubles() {
+  return kYTabRowTables * 64 * R + PFac<R>::kNumFields * 64;
+}
+// stage the tables when tables + two tiles + the exchange scratch fit the 160 KB LDS
+template <int R, typename T, int W>
+constexpr bool kspec_tables_in_lds() {
+  return kspec_lds_tables_doubles<R, T, W>() * 8 + 2 * Stage<R, T, W, 1>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+             kspec_scratch_doubles<R, W>() * 8 <=
+         158 * 1024;
+}
+template <int R, typename T, int W>
+constexpr bool kspec_double_tile() {
+  return (kspec_tables_in_lds<R, T, W>() ? kspec_lds_tables_doubles<R, T, W>() * 8 : 0) +
+             2 * Stage<R, T, W, 1>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+             kspec_scratch_doubles<R, W>() * 8 <=
+         158 * 1024;
+}
+
+// Reference-parity variants (compile-time, PAR bits): kParDD = explicit viscous D2 as D1 o D1
+// (RK3_kernels.cu:160-164, derivatives_nu_double.cu:440-446); kParAnalytic = analytic influence
+// functions (bilplacSolver_double.cu:56-250, l1/l2 typo fixed).  The default (PAR = 0) is the
+// compact D2 and discrete Green's functions; the parity code paths would otherwise set the
+// register allocation of the default kernel.
+constexpr int kParDD = 1, kParAnalytic = 2;
+
+template <int R, typename T, int W, int NS, int XM, int PAR>
+__global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
+  using T2 = typename Cplx<T>::type;
+  using St = Stage<R, T, W, NS>;
+  constexpr int ROWS = 64 * R;
+  constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
+  constexpr int NTAB = kspec_lds_tables_doubles<R, T, W>();
+  constexpr bool kDoubleTile = kspec_double_tile<R, T, W>();
+  constexpr int XS = xl_scratch_doubles(kKspecXK);
+  __shared__ double tab_lds[TLDS ? NTAB : 1];
+  __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * St::TILE];
+  __shared__ double xs_mem[kspec_scratch_doubles<R, W>()];
+  const int lane = __lane_id();
+  const int w = threadIdx.x / 64;
+  const int N = a.N;
+  if constexpr (TLDS) {
+    // coefficient tables (13 per-row tables + the D1 factorisation, contiguous from d1_lo) staged
+    // once per block: every solve step reads them, and from L2 each read is a dependent load
+    const double* src = tg.d1_lo;
+    for (int i = threadIdx.x; i < NTAB; i += W * 64) tab_lds[i] = src[i];
+  }
+  // Table pointers re-derived at each phase from a laundered zero offset: the table reads are
+  // loop-invariant, and without this LICM/GVN hoist every one of them out of the tile loop and
+  // keep them live across all phases (13 tables x R + the D1 factor: ~260 registers at R = 7).
+  // Within a phase the compiler still shares and schedules them freely.
+  YTab t = tg;
+  auto fresh = [&]() {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    if constexpr (TLDS) {
+      const double* b = tab_lds + z;
+      t.d1_lo = b + 0 * ROWS;
+      t.d1_up = b + 1 * ROWS;
+      t.d1_rm = b + 2 * ROWS;
+      t.d1_rc = b + 3 * ROWS;
+      t.d1_rp = b + 4 * ROWS;
+      t.m_lo = b + 5 * ROWS;
+      t.m_up = b + 6 * ROWS;
+      t.k_lo = b + 7 * ROWS;
+      t.k_c = b + 8 * ROWS;
+      t.k_up = b + 9 * ROWS;
+      t.mask = b + 10 * ROWS;
+      t.d1row0 = b + 11 * ROWS;
+      t.d1rowN = b + 12 * ROWS;
+      t.d1fac = b + kYTabRowTables * ROWS;
+    } else {
+      t.d1_lo = tg.d1_lo + z;
+      t.d1_up = tg.d1_up + z;
+      t.d1_rm = tg.d1_rm + z;
+      t.d1_rc = tg.d1_rc + z;
+      t.d1_rp = tg.d1_rp + z;
+      t.m_lo = tg.m_lo + z;
+      t.m_up = tg.m_up + z;
+      t.k_lo = tg.k_lo + z;
+      t.k_c = tg.k_c + z;
+      t.k_up = tg.k_up + z;
+      t.mask = tg.mask + z;
+      t.d1row0 = tg.d1row0 + z;
+      t.d1rowN = tg.d1rowN + z;
+      t.d1fac = tg.d1fac + z;
+    }
+  };
+  // zero tiles: rows >= N stay zero for the whole kernel (Stage::commit)
+  for (int i = threadIdx.x; i < (kDoubleTile ? 2 : 1) * St::TILE; i += W * 64) tile_mem[i] = T2{0, 0};
+  __syncthreads();
+  const Xl<XM> xl{xs_mem + w * XS};
+  // statistics reduction [4][64 R] in the staging tiles: between the phi store and the output
+  // stores nothing reads them, and the output stores rewrite every slot a column read uses
+  // (padding rows included, with zeros) before the next staging
+  double* sred = reinterpret_cast<double*>(tile_mem);
+  static_assert(St::TILE * sizeof(T2) >= 4 * ROWS * sizeof(double), "tile too small for the statistics reduction");
+
+  // Persistent blocks: the grid is the resident capacity and each block walks tiles of W lines.
+  // XCD-aware order: at each iteration the blocks of one XCD take consecutive tiles, which share
+  // partial 128-B lines in that L2.
+  const int ntiles = (a.lines + W - 1) / W;
+  const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
+  T2* phi = static_cast<T2*>(a.phi);
+  T2* omega = static_cast<T2*>(a.omega);
+  T2* Rphi = static_cast<T2*>(a.Rphi);
+  T2* Romega = static_cast<T2*>(a.Romega);
+  const bool zprev = a.rk_z != 0.0;
+  // input sequence of mode 1: 0 H_x, 1 H_z, 2 H_y, 3 phi, 4 omega, 5 R_phi, 6 R_omega (5, 6 only
+  // when the substep uses the previous nonlinear term); input i goes to slot i % NS and is
+  // prefetched when input i - NS is committed
+  constexpr int D = NS;
+  const int nin = zprev ? 7 : 5;
+  auto src_of = [&](int i) -> const T2* {
+    switch (i) {
+      case 0: return static_cast<const T2*>(a.out[0]);
+      case 1: return static_cast<const T2*>(a.out[2]);
+      case 2: return static_cast<const T2*>(a.out[1]);
+      case 3: return phi;
+      case 4: return omega;
+      case 5: return Rphi;
+      default: return Romega;
+    }
+  };
+  auto ahead = [&](auto ic, int l0) {
+    constexpr int I = decltype(ic)::value;
+    if constexpr (I < 7) {
+      if (I < nin) st.template prefetch_at<I % NS>(src_of(I), l0);
+    }
+  };
+  if (a.mode == 1 && lb < ntiles) {
+    ahead(std::integral_constant<int, 0>{}, lb * W);
+    if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, lb * W);
+  }
+  // optional per-phase shader-clock accounting (CHANNEL_KSPEC_PROF)
+  const bool prof_on = a.prof != nullptr;
+  unsigned long long tprev = prof_on ? __builtin_amdgcn_s_memtime() : 0;
+#define KSPEC_STAMP(k)                                            \
+  if (prof_on) {                                                  \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    if (lane == 0) atomicAdd(&a.prof[k], now_ - tprev);           \
+    tprev = now_;                                                 \
+  }
+  for (int tile = lb; tile < ntiles; tile += gridDim.x) {
+    const int line0 = tile * W;
+    st.set_line0(line0);
+    const int line = line0 + w;
+    const bool valid = line < a.lines;
+    const int next_line0 = (tile + static_cast<int>(gridDim.x)) * W;
+    const bool has_next = a.mode == 1 && next_line0 < a.lines;
+
+    const int ikx = valid ? line / a.nkz : 0;
+    const int kz = valid ? a.kz0 + (line - ikx * a.nkz) : 0;
+    const int ig = a.kx0 + ikx;
+    const int kx = ig <= a.Kx ? ig : ig - a.nkx;
+    const double al = a.ax * kx, be = a.az * kz;
+    const double k2 = al * al + be * be;
+    const bool is_mean = valid && kx == 0 && kz == 0;
+    const double inv_k2 = k2 > 0.0 ? 1.0 / k2 : 0.0;
+    // the mean line (al = be = 0) differs only by these terms: wave-uniform multipliers instead
+    // of per-element selects
+    const double mf = is_mean ? 1.0 : 0.0;
+
+    double ph[2][R];  // phi (state)
+    double vo[4][R];  // v (0, 1) and omega (2, 3; U(y) on the mean line): the final D1's operands
+    double mean_diag_flux = 0.0, mean_C = 0.0;
+
+    if (a.mode == 1) {
+      const double dt = *a.dt;
+      double RPn[2][R], RWn[2][R];
+      fresh();
+      // ---------------- nonlinear terms h_v, h_g in M-form ---------------------------------
+      {
+        double X[2][R], G[2][R];
+        {
+          double H[2][R];
+          st.template commit<0 % NS>(H);  // H_x
+          ahead(std::integral_constant<int, D>{}, line0);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            X[0][r] = al * H[1][r];  // -i al Hx
+            X[1][r] = -al * H[0][r];
+            G[0][r] = mf * H[0][r] - be * H[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
+            G[1][r] = be * H[0][r];
+          }
+          st.template commit<1 % NS>(H);  // H_z
+          ahead(std::integral_constant<int, 1 + D>{}, line0);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            X[0][r] += be * H[1][r];  // -i be Hz
+            X[1][r] -= be * H[0][r];
+            G[0][r] += al * H[1][r];  // -i al Hz
+            G[1][r] -= al * H[0][r];
+          }
+        }
+        double Y[2][R];
+        fresh();
+        d1_apply_to<R, 2, XM>(t, X, Y, xl, lane);  // D(-i al Hx - i be Hz)
+        st.template commit<2 % NS>(X);              // H_y (X is free)
+        ahead(std::integral_constant<int, 2 + D>{}, line0);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) Y[k][r] -= k2 * X[k][r];
+        fresh();
+        apply_M<R, 2, XM>(t, Y, RPn, lane);
+        apply_M<R, 2, XM>(t, G, RWn, lane);
+        KSPEC_STAMP(0)
+        if (a.mean_diag && is_mean) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = lane * R + r;
+            if (j < N) a.mean_diag[N + j] = G[0][r];
+          }
+        }
+      }
+      // ---------------- explicit part of the RK3 substep in M-form -------------------------
+      // M rhs = M q + dt [ a_n nu (K q - k^2 M q) + g_n R_now + z_n R_prev ]
+      double rhsP[2][R], rhsW[2][R];
+      {
+        const double cM = 1.0 - dt * a.rk_a * a.nu * k2, cK = dt * a.rk_a * a.nu, cg = dt * a.rk_g;
+        auto explicit_op = [&](const double (&q)[2][R], double (&o)[2][R]) {
+          if ((PAR & kParDD) && !is_mean) {
+            // reference parity (RK3_kernels.cu:160-164, derivatives_nu_double.cu:440-446): the
+            // explicit viscous D2 of the fluctuations as D1 o D1, M (cM q + cK D1 D1 q)
+            double D1q[2][R], DD[2][R];
+            d1_apply_to<R, 2, XM>(t, q, D1q, xl, lane);
+            d1_apply_to<R, 2, XM>(t, D1q, DD, xl, lane);
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+              for (int r = 0; r < R; ++r) DD[k][r] = cM * q[k][r] + cK * DD[k][r];
+            apply_M<R, 2, XM>(t, DD, o, lane);
+          } else {
+            apply_tri2<R, 2, XM>(t.m_lo, t.mask, t.m_up, cM, t.k_lo, t.k_c, t.k_up, cK, q, o, lane);
+          }
+        };
+        double q[2][R];
+        fresh();
+        st.template commit<3 % NS>(q);  // phi
+        ahead(std::integral_constant<int, 3 + D>{}, line0);
+        explicit_op(q, rhsP);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsP[k][r] += cg * RPn[k][r];
+        fresh();
+        st.template commit<4 % NS>(q);  // omega
+        ahead(std::integral_constant<int, 4 + D>{}, line0);
+        explicit_op(q, rhsW);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsW[k][r] += cg * RWn[k][r];
+        if (zprev) {
+          const double cz = dt * a.rk_z;
+          st.template commit<5 % NS>(q);  // R_phi
+          ahead(std::integral_constant<int, 5 + D>{}, line0);
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int r = 0; r < R; ++r) rhsP[k][r] += cz * q[k][r];
+          st.template commit<6 % NS>(q);  // R_omega
+#pragma unroll
+          for (int k = 0; k < 2; ++k)
+#pragma unroll
+            for (int r = 0; r < R; ++r) rhsW[k][r] += cz * q[k][r];
+        }
+      }
+      KSPEC_STAMP(1)
+      st.store(Rphi, RPn);
+      st.store(Romega, RWn);
+      KSPEC_STAMP(2)
+
+      // ---------------- implicit viscous solves (phi, omega share one factorisation) -------
+      const double c = a.rk_b * dt * a.nu;
+      double pp[4][R];  // phi particular (0, 1) and the two homogeneous phi solutions (2, 3)
+      fresh();
+      {
+        PFac<R> F;
+        const CoefImpl ci{t, lane, 1.0 + c * k2, c};
+        pfactor<R, XM>(F, ci, xl, lane);
+        {
+          // omega, phi and the two homogeneous phi solutions (k=0 -> phi(-1)=1, k=1 -> phi(+1)=1)
+          // share the factorisation: one solve with 6 real right-hand sides
+          double Z[6][R];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = lane * R + r;
+            Z[0][r] = rhsW[0][r];
+            Z[1][r] = rhsW[1][r];
+            Z[2][r] = rhsP[0][r];
+            Z[3][r] = rhsP[1][r];
+            Z[4][r] = (j == 0) ? 1.0 : 0.0;
+            Z[5][r] = (j == N - 1) ? 1.0 : 0.0;
+          }
+          psolve<R, 6, XM>(F, ci, Z, xl, lane);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            rhsW[0][r] = Z[0][r];
+            rhsW[1][r] = Z[1][r];
+            pp[0][r] = Z[2][r];
+            pp[1][r] = Z[3][r];
+            pp[2][r] = Z[4][r];
+            pp[3][r] = Z[5][r];
+          }
+        }
+        if (is_mean) {
+          // constant flow rate: U += C * U1, U1 = response to a unit mean pressure gradient
+          double fU = 0.0;
+#pragma unroll
+          for (int r = 0; r < R; ++r) fU += tab(t.trap, r, lane) * rhsW[0][r];
+          fU = wave_sum<XM>(fU);
+          if (a.forcing == 0) {
+            double one[1][R], U1[1][R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) one[0][r] = (lane * R + r < N) ? 1.0 : 0.0;
+            apply_tri<R, 1, XM>(t.m_lo, t.mask, t.m_up, one, U1, lane);
+            psolve<R, 1, XM>(F, ci, U1, xl, lane);
+            double f1 = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) f1 += tab(t.trap, r, lane) * U1[0][r];
+            f1 = wave_sum<XM>(f1);
+            mean_C = f1 != 0.0 ? (a.Q - fU) / f1 : 0.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) rhsW[0][r] += mean_C * U1[0][r];
+          } else {
+            // reference forcing (meanUevol.c:201-221): constant added to interior points
+            mean_C = (a.Q - fU) / 2.0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) rhsW[0][r] += mean_C * tab(t.mask, r, lane);
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) rhsW[1][r] = 0.0;
+          mean_diag_flux = fU;
+        }
+      }
+      KSPEC_STAMP(3)
+      st.store(omega, rhsW);
+      KSPEC_STAMP(4)
+
+      // ---------------- velocity recovery + influence matrix (v(+-1) = v'(+-1) = 0) --------
+      fresh();
+      {
+        PFac<R> F;
+        const CoefHelm chm{t, lane, k2};
+        pfactor<R, XM>(F, chm, xl, lane);
+        double Y[4][R];  // v particular (0, 1), homogeneous v (2, 3)
+        apply_M<R, 4, XM>(t, pp, Y, lane);
+        psolve<R, 4, XM>(F, chm, Y, xl, lane);
+        fresh();
+        // wall derivatives v'(+-1) = first / last row of the dense D1 applied to v (no solves)
+        double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double g0 = tab(t.d1row0, r, lane), gN = tab(t.d1rowN, r, lane);
+          acc[0] += g0 * Y[0][r];
+          acc[1] += g0 * Y[1][r];
+          acc[2] += gN * Y[0][r];
+          acc[3] += gN * Y[1][r];
+          acc[4] += g0 * Y[2][r];
+          acc[5] += gN * Y[2][r];
+          acc[6] += g0 * Y[3][r];
+          acc[7] += gN * Y[3][r];
+        }
+        wave_sum_n<8, XM>(acc);
+        const double p0r = acc[0], p0i = acc[1], pNr = acc[2], pNi = acc[3];
+        double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
+        if ((PAR & kParAnalytic) && k2 > 0.0 && dt > 1e-14) {
+          // reference parity (bilplacSolver_double.cu:56-217): phi1,2 = (C_l1 -+ S_l1)/2,
+          // v1,2 = D [(C_l1 -+ S_l1)/2 - (C_l2 -+ S_l2)/2], l1^2 = k^2 + Re/(beta dt), l2 = k,
+          // D = 1/(l1^2 - l2^2); wall derivatives analytic, the particular one discrete
+          const double l2 = sqrt(k2), l1 = sqrt(k2 + 1.0 / (a.rk_b * dt * a.nu)), Dd = 1.0 / (l1 * l1 - l2 * l2);
+          double dh[2][2];  // [solution][wall]
+#pragma unroll
+          for (int wall = 0; wall < 2; ++wall) {
+            const double yw = wall == 0 ? -1.0 : 1.0;
+            double C1_, S1_, dC1, dS1, C2_, S2_, dC2, dS2;
+            chs_profiles(l1, yw, C1_, S1_, dC1, dS1);
+            chs_profiles(l2, yw, C2_, S2_, dC2, dS2);
+            dh[0][wall] = Dd * (0.5 * (dC1 - dS1) - 0.5 * (dC2 - dS2));
+            dh[1][wall] = Dd * (0.5 * (dC1 + dS1) - 0.5 * (dC2 + dS2));
+          }
+          h10 = dh[0][0];
+          h1N = dh[0][1];
+          h20 = dh[1][0];
+          h2N = dh[1][1];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = lane * R + r;
+            const bool in = j < N;
+            const double yj = in ? a.ygrid[j] : 0.0;
+            double C1_, S1_, dC1, dS1, C2_, S2_, dC2, dS2;
+            chs_profiles(l1, yj, C1_, S1_, dC1, dS1);
+            chs_profiles(l2, yj, C2_, S2_, dC2, dS2);
+            pp[2][r] = in ? 0.5 * (C1_ - S1_) : 0.0;
+            pp[3][r] = in ? 0.5 * (C1_ + S1_) : 0.0;
+            Y[2][r] = in ? Dd * (0.5 * (C1_ - S1_) - 0.5 * (C2_ - S2_)) : 0.0;
+            Y[3][r] = in ? Dd * (0.5 * (C1_ + S1_) - 0.5 * (C2_ + S2_)) : 0.0;
+          }
+        }
+        const double det = h10 * h2N - h20 * h1N;
+        const bool apply = !is_mean && k2 > 0.0 && dt > 1e-14 && det != 0.0;
+        const double id = apply ? 1.0 / det : 0.0;
+        // [h10 h20; h1N h2N] [C1; C2] = -[p0; pN]
+        const double C1r = (-p0r * h2N + h20 * pNr) * id, C1i = (-p0i * h2N + h20 * pNi) * id;
+        const double C2r = (-h10 * pNr + h1N * p0r) * id, C2i = (-h10 * pNi + h1N * p0i) * id;
+        const double nz = (is_mean || k2 == 0.0) ? 0.0 : 1.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          ph[0][r] = nz * (pp[0][r] + C1r * pp[2][r] + C2r * pp[3][r]);
+          ph[1][r] = nz * (pp[1][r] + C1i * pp[2][r] + C2i * pp[3][r]);
+          vo[0][r] = nz * (Y[0][r] + C1r * Y[2][r] + C2r * Y[3][r]);
+          vo[1][r] = nz * (Y[1][r] + C1i * Y[2][r] + C2i * Y[3][r]);
+        }
+      }
+      KSPEC_STAMP(5)
+      {
+        // omega was the last field staged (store above): re-read it from the tile, not from HBM
+        double om[2][R];
+        st.column(om);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          vo[2][r] = om[0][r];
+          vo[3][r] = om[1][r];
+        }
+      }
+      st.store(phi, ph);
+      KSPEC_STAMP(6)
+      // the next tile's first inputs load during the D1 solve and the output stores
+      if (has_next) {
+        ahead(std::integral_constant<int, 0>{}, next_line0);
+        if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
+      }
+    } else {
+      // ---------------- prepare only: fields from the state --------------------------------
+      fresh();
+      double om[2][R];
+      st.load(phi, ph);
+      st.load(omega, om);
+      PFac<R> F;
+      const CoefHelm chm{t, lane, k2};
+      pfactor<R, XM>(F, chm, xl, lane);
+      double v[2][R];
+      apply_M<R, 2, XM>(t, ph, v, lane);
+      psolve<R, 2, XM>(F, chm, v, xl, lane);
+      const double nz = (is_mean || k2 == 0.0) ? 0.0 : 1.0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ph[0][r] = nz * ph[0][r];
+        ph[1][r] = nz * ph[1][r];
+        vo[0][r] = nz * v[0][r];
+        vo[1][r] = nz * v[1][r];
+        vo[2][r] = om[0][r];
+        vo[3][r] = om[1][r];
+      }
+    }
+
+    // ---------------- health check (non-finite state) ---------------------------------------
+    if (a.health) {
+      bool bad = false;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        bad |= !isfinite(ph[0][r]) || !isfinite(ph[1][r]) || !isfinite(vo[2][r]) || !isfinite(vo[3][r]);
+      if (__any(bad) && lane == 0) atomicOr(a.health, 1u);
+    }
+
+    // ---------------- prepare velocity / vorticity for the physical-space stage --------------
+    fresh();
+    double dvo[4][R];  // D1 v (0, 1), D1 omega (2, 3): one 4-RHS solve
+    d1_apply_to<R, 4, XM>(t, vo, dvo, xl, lane);
+    KSPEC_STAMP(7)
+    // velocities u = i (al dv - be om)/k2, w = i (be dv + al om)/k2 (nonLinear_kernels.cu:55-72),
+    // formed one output at a time (each is stored before the next is built)
+    auto vel_u = [&](int r, double& re, double& im) {
+      const double ar = (al * dvo[0][r] - be * vo[2][r]) * inv_k2, ai = (al * dvo[1][r] - be * vo[3][r]) * inv_k2;
+      re = mf * vo[2][r] - ai;  // mean line: U(y)
+      im = ar;
+    };
+    auto vel_w = [&](int r, double& re, double& im) {
+      const double br = (be * dvo[0][r] + al * vo[2][r]) * inv_k2, bi = (be * dvo[1][r] + al * vo[3][r]) * inv_k2;
+      re = -bi;
+      im = br;
+    };
+    // plane statistics (statistics.cu:7-95), fluctuations only, weight 2 for kz > 0
+    if (a.stats) {
+      __syncthreads();  // every wave is done with the tiles (last staging: the phi store)
+      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) sred[i] = 0.0;
+      __syncthreads();
+      if (valid && !is_mean) {
+        const double wgt = kz == 0 ? 1.0 : 2.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int idx = r * 64 + lane;
+          double ur, ui, wr, wi;
+          vel_u(r, ur, ui);
+          vel_w(r, wr, wi);
+          atomicAdd(&sred[0 * ROWS + idx], wgt * (ur * ur + ui * ui));
+          atomicAdd(&sred[1 * ROWS + idx], wgt * (vo[0][r] * vo[0][r] + vo[1][r] * vo[1][r]));
+          atomicAdd(&sred[2 * ROWS + idx], wgt * (wr * wr + wi * wi));
+          atomicAdd(&sred[3 * ROWS + idx], wgt * (ur * vo[0][r] + ui * vo[1][r]));
+        }
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) {
+        const int s = i / ROWS, rem = i - s * ROWS, r = rem / 64, l = rem - r * 64;
+        const int j = l * R + r;
+        if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
+      }
+      __syncthreads();  // sred is a staging tile again
+    }
+    KSPEC_STAMP(8)
+    st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);                   // v
+    st.store(static_cast<T2*>(a.out[4]), vo[2], vo[3], 1.0 - mf);         // omega_y (0 on the mean line)
+    {
+      double x[2][R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
+      st.store(static_cast<T2*>(a.out[0]), x);
+#pragma unroll
+      for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
+      st.store(static_cast<T2*>(a.out[2]), x);
+      // vorticity: wx = Dw - i be v ; wz = i al v - Du   (convolution_kernels.cu:46-53)
+      // D(dv) = D2 v = phi + k2 v (Helmholtz identity, consistent with the compact D2 operator)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+        const double br = (be * DDr + al * dvo[2][r]) * inv_k2, bi = (be * DDi + al * dvo[3][r]) * inv_k2;
+        x[0][r] = -bi + be * vo[1][r];
+        x[1][r] = br - be * vo[0][r];
+      }
+      st.store(static_cast<T2*>(a.out[3]), x);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+        const double ar = (al * DDr - be * dvo[2][r]) * inv_k2, ai = (al * DDi - be * dvo[3][r]) * inv_k2;
+        // Du = i(ar + i ai) = -ai + i ar ; wz = i al v - Du ; mean line: -dU/dy
+        x[0][r] = -al * vo[1][r] + ai - mf * dvo[2][r];
+        x[1][r] = al * vo[0][r] - ar;
+      }
+      st.store(static_cast<T2*>(a.out[5]), x);
+    }
+    if (a.mean_diag && is_mean) {
+      const double d0 = row_value<R, XM>(dvo[2], 0, lane), dN = row_value<R, XM>(dvo[2], N - 1, lane);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = lane * R + r;
+        if (j < N) a.mean_diag[j] = vo[2][r];
+      }
+      if (lane == 0) {
+        a.mean_diag[3 * N + 0] = d0;
+        a.mean_diag[3 * N + 1] = dN;
+        a.mean_diag[3 * N + 2] = mean_diag_flux;
+        a.mean_diag[3 * N + 3] = mean_C;
+      }
+    }
+    KSPEC_STAMP(9)
+  }  // tile loop
+#undef KSPEC_STAMP
+}
+
+template <int R, typename T, int PAR = 0>
+static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
+  constexpr int W = kspec_lines<R, T>();
+  auto kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR>;
+  // persistent grid: as many blocks as can be resident at once
+  const int ntiles = (a.lines + W - 1) / W;
+  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), W * 64))), block(W * 64);
+  hipLaunchKernelGGL(kern, grid, block, 0, stream, t.tab, a);
+}
+
+// all rows-per-lane and storage instantiations of one parity variant
+template <int PAR>
+void kspec_launch_par(const YTablesDev& t, const SpecArgs& a, bool fp64, hipStream_t stream) {
+#ifdef CH_KSPEC_ISA_ONLY  // one instantiation, for ISA inspection builds
+  CH_CHECK(t.R == CH_KSPEC_ISA_ONLY && !fp64, "ISA build");
+  kspec_launch_t<CH_KSPEC_ISA_ONLY, float, PAR>(t, a, stream);
+#else
+  if (fp64) {
+    CH_DISPATCH_R(t.R, (kspec_launch_t<R, double, PAR>(t, a, stream)));
+  } else {
+    CH_DISPATCH_R(t.R, (kspec_launch_t<R, float, PAR>(t, a, stream)));
+  }
+#endif
+}
+extern template void kspec_launch_par<0>(const YTablesDev&, const SpecArgs&, bool, hipStream_t);
+extern template void kspec_launch_par<1>(const YTablesDev&, const SpecArgs&, bool, hipStream_t);
+extern template void kspec_launch_par<2>(const YTablesDev&, const SpecArgs&, bool, hipStream_t);
+extern template void kspec_launch_par<3>(const YTablesDev&, const SpecArgs&, bool, hipStream_t);
+
+}  // namespace channel

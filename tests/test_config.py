@@ -64,8 +64,10 @@ def test_file_and_example(native):
     assert c.NX == 128 and c.nsteps == 100 and c.out_G == "G.h5"
 
 
-@pytest.mark.parametrize("bad", ["NX = 100; NY = 33; NZ = 17;",      # NX not a power of two
-                                 "NX = 64; NY = 33; NZ = 16;",       # 2NZ-2 not a power of two
+@pytest.mark.parametrize("bad", ["NX = 100; NY = 33; NZ = 17;",      # NX not 2^k, 3*2^k or 5*2^k
+                                 "NX = 64; NY = 33; NZ = 16;",       # 2NZ-2 = 30 likewise
+                                 "NX = 24; NY = 33; NZ = 17;",       # 3*2^k below 48
+                                 "NX = 3072; NY = 33; NZ = 17;",     # above the largest kernel
                                  "NX = 64; NY = 3; NZ = 17;",        # NY too small
                                  "NX = 64; NY = 33; NZ = 17; precision = \"bf16\";",
                                  "NX = 64 NY = 33;",                 # syntax
@@ -73,6 +75,14 @@ def test_file_and_example(native):
 def test_invalid(native, bad):
     with pytest.raises(RuntimeError):
         native.Config.from_string(bad)
+
+
+@pytest.mark.parametrize("nx,nz", [(96, 97), (192, 49), (384, 193), (768, 385), (1536, 769), (80, 81), (1280, 641),
+                                   (48, 25), (2048, 1025)])
+def test_non_power_of_two_lengths(native, nx, nz):
+    """Grids of the form 3*2^k and 5*2^k (cuFFT plans of any length in the reference, fft.c:17-23)."""
+    c = native.Config.from_string(f"NX = {nx}; NY = 33; NZ = {nz};")
+    assert c.NX == nx and c.NZ == nz
 
 
 def test_input_files_imply_file_ic(native):

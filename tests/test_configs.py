@@ -44,3 +44,14 @@ def test_config_parses_and_plans(native, path):
             assert p.R * 64 >= NY
         p0 = native.Plan.make(c, P, 0)
         assert lines == p0.nkx * p0.nkz
+
+
+@pytest.mark.parametrize("preset,conf", [("retau180", "retau180_128x129x128"), ("retau550", "retau550_512x257x512"),
+                                         ("retau950", "retau950_1024x385x1024"), ("retau2000", "retau2000_2048x633x2048")])
+def test_presets_match_shipped_configs(native, preset, conf):
+    """The Python presets and the configs/*.conf files name the same physical case."""
+    from channel_gpu_amd.utils.config import load_config, reference_preset
+
+    p = reference_preset(preset)
+    c = load_config(os.path.join(ROOT, "configs", conf + ".conf"))
+    assert (p.NX, p.NY, p.NZ, p.Re, p.Q) == (c.NX, c.NY, c.NZ, c.Re, c.Q)

@@ -55,9 +55,11 @@ def test_d1_dense_mfma(native, NY):
     assert rel(got, ora.op_d1(ops, x)) < 1e-10
 
 
-@pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048])
+@pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048,
+                               48, 96, 192, 384, 768, 1536, 80, 160, 320, 640, 1280])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_fft_c2c(native, n, dtype):
+    """Batched C2C against numpy, powers of two and the radix-3 / radix-5 plans (3*2^k, 5*2^k)."""
     rng = np.random.default_rng(n)
     x = rng.standard_normal((7, n)) + 1j * rng.standard_normal((7, n))
     xt = torch.tensor(x, dtype=dtype, device=DEV)
@@ -68,7 +70,8 @@ def test_fft_c2c(native, n, dtype):
     assert rel(fwd, np.fft.fft(x, axis=-1)) < tol * np.log2(n)
 
 
-@pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20), (2048, 9)])
+@pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20), (2048, 9),
+                                    (96, 13), (192, 11), (384, 20), (768, 9), (1536, 5), (80, 7), (1280, 6)])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_xfft(native, NX, nkz, dtype):
     rng = np.random.default_rng(NX)
@@ -91,7 +94,12 @@ def test_xfft(native, NX, nkz, dtype):
 @pytest.mark.parametrize("NX,Nzp,dtype", [(32, 32, torch.complex128), (64, 128, torch.complex64),
                                           (16, 1024, torch.complex64), (16, 1024, torch.complex128),
                                           (32, 2048, torch.complex64), (8, 2048, torch.complex128),
-                                          (16, 512, torch.complex128)])
+                                          (16, 512, torch.complex128),
+                                          (16, 96, torch.complex64), (8, 192, torch.complex128),
+                                          (8, 384, torch.complex64), (4, 768, torch.complex64),
+                                          (4, 768, torch.complex128), (2, 1536, torch.complex64),
+                                          (4, 1536, torch.complex128), (4, 1280, torch.complex64),
+                                          (8, 160, torch.complex128)])
 def test_zphys(native, NX, Nzp, dtype):
     """z stage vs NumPy (LDS-pass kernel; the register-resident one is covered in a subprocess)."""
     rng = np.random.default_rng(Nzp)

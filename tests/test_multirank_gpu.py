@@ -86,6 +86,11 @@ def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mo
         ref.step()
     shm = f"shm:chtest_{uuid.uuid4().hex[:12]}"
     with tempfile.TemporaryDirectory() as d:
+        # a turn marker left behind by a crashed earlier run of the same checkpoint path, in the
+        # pre-nonce format "<serial> <turn>": it must not let rank 1 start writing before rank 0 has
+        # created the file (the planes of rank 1 would be lost without an error)
+        with open(os.path.join(d, "Ga.h5.turn"), "w") as f:
+            f.write("1 1\n")
         mp.start_processes(_worker, args=(world, shm, d, nsteps, pr), nprocs=world, join=True,
                            start_method="spawn")
         parts = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
@@ -108,12 +113,23 @@ def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mo
 
             cfg = default_config(**GRID, Re=400.0, precision="fp64", ic="zero", stats_every=0, log_every=0)
             s1 = native.Solver(cfg, 0, 1, 0, b"")
-            s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), os.path.join(d, "U.bin"))
+            # no UMEAN file named: U from the full-precision 'umean' dataset of the G file
+            s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), "-")
             rphi, rom, rU = s1.get_state()
             gphi, gom = _assemble(parts, "phi"), _assemble(parts, "om")
             # fp64 storage writes float64 datasets and U at full precision: exact
             assert np.array_equal(rphi, gphi) and np.array_equal(rom, gom)
             assert np.abs(rU - ref.U).max() < 1e-11
+            # the companion UMEAN file (float32 records of the same profile): the full-precision copy
+            s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), os.path.join(d, "U.bin"))
+            assert np.array_equal(s1.get_state()[2], rU)
+            # an edited UMEAN file wins over the profile stored in G
+            u_edit = np.fromfile(os.path.join(d, "U.bin"), dtype=np.float32)
+            u_edit[2 * (len(u_edit) // 4)] *= 1.5  # U of the middle row (records are float32 pairs)
+            u_edit.tofile(os.path.join(d, "U2.bin"))
+            s1.read_restart(os.path.join(d, "G.h5"), os.path.join(d, "DDV.h5"), os.path.join(d, "U2.bin"))
+            fU = s1.get_state()[2]
+            assert not np.array_equal(fU, rU) and np.abs(fU - rU).max() > 0.1 * np.abs(rU).max()
             # the background writer (ranks passing the file by marker files) wrote the same data
             s2 = native.Solver(cfg, 0, 1, 0, b"")
             s2.read_restart(os.path.join(d, "Ga.h5"), os.path.join(d, "DDVa.h5"), "-")
