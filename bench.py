@@ -43,6 +43,11 @@ RE_TAU_LABEL = {(32, 33, 32): "laminar Poiseuille", (128, 129, 128): "Re_tau~180
 # environment switches that skip work inside the timed region (diagnosis only)
 WORK_SKIPPING_ENV = ("CHANNEL_FFT_DIAG",)
 HEADLINE_METRIC = "wall-sec/RK3-step + grid-pts/sec at Re_tau=950, 1024x385x1024, 1/2/4/8 GPU"
+# statistics cadence of the reference (FREC_STATS = 10, channel.h:82; computed in nonLinear.c:11-12):
+# every 10th timed step also accumulates the plane statistics in its last substep
+STATS_EVERY = 10
+# xGMI model: one link per peer pair, ~153 GB/s per link (point-to-point, no switch)
+XGMI_LINK_GBPS = 153.0
 PHASES = ["kspec", "x_backward", "z_physical", "x_forward", "a2a", "reduce", "io", "other"]
 
 
@@ -83,6 +88,8 @@ def main() -> None:
     ap.add_argument("--phases", action="store_true",
                     help="after the timed steps, time a few more eagerly with per-phase hipEvents")
     ap.add_argument("--phase-steps", type=int, default=3)
+    ap.add_argument("--stats-every", type=int, default=STATS_EVERY,
+                    help="plane statistics every k-th step inside the timed region (0 = never)")
     args = ap.parse_args()
 
     bad = [e for e in WORK_SKIPPING_ENV if os.environ.get(e, "0") not in ("", "0")]
@@ -95,7 +102,7 @@ def main() -> None:
     # the native TCP rendezvous hands out the communicator id
     os.environ["CHANNEL_TORCH_FREE"] = "1"
     from channel_gpu_amd import require_core
-    from channel_gpu_amd.parallel.decomposition import SlabDecomposition
+    from channel_gpu_amd.parallel.decomposition import PencilDecomposition, SlabDecomposition
     from channel_gpu_amd.parallel.native_bootstrap import init_native
     from channel_gpu_amd.utils.config import default_config
 
@@ -120,13 +127,16 @@ def main() -> None:
     def max_over_ranks(x: float) -> float:
         return float(solver.max_over_ranks(float(x)))
 
-    for _ in range(args.warmup):
-        solver.step(False)
+    se = max(0, args.stats_every)
+    # the warm-up captures both step graphs (with and without the statistics pass) when it has at
+    # least two steps, so no capture falls inside the timed region
+    for i in range(args.warmup):
+        solver.step(se > 0 and args.warmup >= 2 and i == args.warmup - 1)
     barrier()
     solver.set_step_timing(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        solver.step(False)
+    for i in range(args.steps):
+        solver.step(se > 0 and (i + 1) % se == 0)
     barrier()
     dt_wall = max_over_ranks(time.perf_counter() - t0)
     step_ms = solver.step_times_ms()
@@ -152,9 +162,21 @@ def main() -> None:
     pts = NX * NY * NZP
     value = pts / s_per_step
     floor = REF_MODEL_FLOOR_S.get(world) if (NX, NY, NZP) == (1024, 385, 1024) else None
+    parallelism = f"slab{world}" if solver.plan.Pr == 1 else f"pencil{solver.plan.Pr}x{solver.plan.Pc}"
+    headline = (NX, NY, NZP) == (1024, 385, 1024) and args.precision == "fp32" and solver.plan.Pr == 1
+    if headline:
+        metric = HEADLINE_METRIC
+    else:
+        why = []
+        if (NX, NY, NZP) != (1024, 385, 1024):
+            why.append("not the headline grid")
+        if args.precision != "fp32":
+            why.append(f"{args.precision} storage")
+        if solver.plan.Pr != 1:
+            why.append(f"{parallelism} decomposition")
+        metric = f"wall-sec/RK3-step + grid-pts/sec at {NX}x{NY}x{NZP} ({', '.join(why)})"
     out = {
-        "metric": (HEADLINE_METRIC if (NX, NY, NZP) == (1024, 385, 1024)
-                   else f"wall-sec/RK3-step + grid-pts/sec at {NX}x{NY}x{NZP} (not the headline grid)"),
+        "metric": metric,
         "value": value,
         "unit": "grid-pts/s",
         "n_gpus": world,
@@ -175,19 +197,33 @@ def main() -> None:
             "grid": f"{NX}x{NY}x{NZP}",
             "global_batch": 1,
             "seq_len": pts,
-            "parallelism": (f"slab{world}" if solver.plan.Pr == 1
-                            else f"pencil{solver.plan.Pr}x{solver.plan.Pc}"),
+            "parallelism": parallelism,
+            "stats_every": se,
             "hipgraph": graph,
             "comm": solver.comm_kind(),
         },
         "health": int(L.health),
         "dt": L.dt,
     }
+    esz = 16 if args.precision == "fp64" else 8
+    if world > 1:
+        # exchange model: the busiest peer pair's bytes per step over one xGMI link
+        if solver.plan.Pr == 1:
+            dec = SlabDecomposition(NX, NY, NZP // 2 + 1, world)
+            peer = max(max(b for q, b in enumerate(dec.a2a_bytes_per_peer_per_step(r, esz)) if q != r)
+                       for r in range(world))
+        else:
+            pd = PencilDecomposition(NX, NY, NZP // 2 + 1, solver.plan.Pr, solver.plan.Pc)
+            peer = 0
+            for r in range(world):
+                eb = pd.exchange_bytes_per_substep(r, esz)
+                peer = max(peer, 3 * max(eb["A"] // max(1, pd.Pc - 1), eb["B"] // max(1, pd.Pr - 1) if pd.Pr > 1 else 0))
+        out["a2a_model_bytes_per_peer_per_step"] = int(peer)
+        out["a2a_model_ms_per_step"] = round(peer / (XGMI_LINK_GBPS * 1e9) * 1e3, 4)
     if phase is not None:
         out["phase_ms_per_step"] = {k: round(v, 4) for k, v in zip(PHASES, phase) if v > 0}
         out["phase_sum_ms_compute"] = round(sum(phase[i] for i in (0, 1, 2, 3)), 4)
         if solver.comm_kind() != "none" and solver.plan.Pr == 1:
-            esz = 16 if args.precision == "fp64" else 8
             dec = SlabDecomposition(NX, NY, NZP // 2 + 1, world)
             per_peer = [b for q, b in enumerate(dec.a2a_bytes_per_peer_per_step(rank, esz)) if q != rank or world == 1]
             a2a_ms = phase[4]

@@ -259,8 +259,10 @@ void Solver::free_all() {
   ev_cb_.clear();
   ev_cc_.clear();
   step_ev_.clear();
-  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_})
+  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_, ev_tdt_[0], ev_tdt_[1]})
     if (e) (void)hipEventDestroy(e);
+  if (h_tdt_) (void)hipHostFree(h_tdt_);
+  h_tdt_ = nullptr;
   for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_, static_cast<void*>(d_y_)})
     if (p) (void)hipFree(p);
   state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = d_sym_ = nullptr;
@@ -343,6 +345,17 @@ void Solver::init_ic() {
     la[N - 1] = grid_.d2_wN_lo;
     std::vector<std::complex<double>> v(N), w(N);
     const double amp = cfg_.ic_amplitude;
+    // smooth in y: each line's profile is a random combination of the Chebyshev polynomials
+    // T_0 .. T_{M-1} (weights 1/(1+m)) times the wall factors, so phi = D2 v - k2 v is a resolved
+    // field (independent draws per grid point made grid-scale noise that D2 amplified by 1/dy^2)
+    constexpr int kIcModes = 8;
+    std::vector<double> cheb(static_cast<size_t>(N) * kIcModes);
+    for (int j = 0; j < N; ++j) {
+      double* T = &cheb[static_cast<size_t>(j) * kIcModes];
+      T[0] = 1.0;
+      T[1] = y[j];
+      for (int m = 2; m < kIcModes; ++m) T[m] = 2.0 * y[j] * T[m - 1] - T[m - 2];
+    }
     for (int ikx = 0; ikx < p.nkx_loc; ++ikx) {
       const int ig = p.kx0 + ikx;
       const int kx = p.kx_of(ig);
@@ -355,13 +368,22 @@ void Solver::init_ic() {
         const bool cj = (kz == 0 && kx < 0);
         const unsigned long long base =
             (cfg_.seed * 1000003ULL + static_cast<unsigned long long>(std::abs(kx))) * 1000033ULL + kz;
+        std::complex<double> cv[kIcModes], co[kIcModes];
+        for (int m = 0; m < kIcModes; ++m) {
+          const unsigned long long key = base * 4099ULL + m;
+          const double wm = 1.0 / (1.0 + m);
+          cv[m] = wm * std::complex<double>(urand(key * 4 + 0), urand(key * 4 + 1));
+          co[m] = wm * std::complex<double>(urand(key * 4 + 2), urand(key * 4 + 3));
+          if (cj) { cv[m] = std::conj(cv[m]); co[m] = std::conj(co[m]); }
+        }
         for (int j = 0; j < N; ++j) {
-          const unsigned long long key = base * 4099ULL + j;
           const double w1 = 1.0 - y[j] * y[j];
-          std::complex<double> vr(urand(key * 4 + 0), urand(key * 4 + 1));
-          std::complex<double> orr(urand(key * 4 + 2), urand(key * 4 + 3));
-          if (cj) { vr = std::conj(vr); orr = std::conj(orr); }
-          if (kz == 0 && kx == 0) { vr = vr.real(); orr = orr.real(); }
+          const double* T = &cheb[static_cast<size_t>(j) * kIcModes];
+          std::complex<double> vr = 0.0, orr = 0.0;
+          for (int m = 0; m < kIcModes; ++m) {
+            vr += cv[m] * T[m];
+            orr += co[m] * T[m];
+          }
           v[j] = amp * env * w1 * w1 * vr;
           w[j] = amp * env * w1 * orr;
         }
@@ -1046,6 +1068,29 @@ void Solver::wait(hipStream_t s) {
   }
 }
 
+void Solver::wait_event(hipEvent_t e) {
+  if (!comm_) {
+    HIP_CHECK(hipEventSynchronize(e));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int it = 0;; ++it) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) HIP_CHECK(r);
+    if (comm_->async_error()) {
+      comm_->abort();
+      CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (comm_timeout_s_ > 0 && el > comm_timeout_s_) {
+      comm_->abort();
+      CH_CHECK(false, "rank " << plan_.rank << ": no progress for " << comm_timeout_s_ << " s; communicator aborted");
+    }
+    if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 void Solver::synchronize() {
   wait(s_comp_);
   wait(s_comm_);
@@ -1260,6 +1305,7 @@ void Solver::run(long nsteps, bool verbose) {
   if (stats_pending_ && se > 0 && nstep_ % se == 0) write_stats_files(stats());
   stats_pending_ = false;
   if (rb && snap_step_ < 0) take_snapshot();
+  tdt_valid_ = false;  // the state may have been reset or restored since the last run()
   auto t_log = std::chrono::steady_clock::now();
   long s_log = nstep_;
   for (long s = 0; s < nsteps; ++s) {
@@ -1308,10 +1354,33 @@ void Solver::run(long nsteps, bool verbose) {
       if (cfg_.checkpoint_async) checkpoint_async(cfg_.out_G + sfx, cfg_.out_DDV + sfx, um);
       else write_restart(cfg_.out_G + sfx, cfg_.out_DDV + sfx, um);
     }
-    if (cfg_.t_end > 0 && time() >= cfg_.t_end) break;
+    if (cfg_.t_end > 0 && t_end_reached()) break;
   }
   synchronize();
   wait_checkpoint();
+}
+
+// t_end without a host sync per step (which would drain the CPU's run-ahead of the GPU): (dt, time)
+// of every step is copied to pinned memory behind the step, and the decision after step s reads the
+// copy of step s-1, which has finished while step s runs.  Within three steps of t_end it reads the
+// device time synchronously, so the run still stops at the first step whose end time reaches t_end.
+bool Solver::t_end_reached() {
+  if (!h_tdt_) {
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_tdt_), 4 * sizeof(double), hipHostMallocDefault));
+    for (auto& e : ev_tdt_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    tdt_valid_ = false;
+  }
+  const int cur = static_cast<int>(nstep_ & 1);
+  HIP_CHECK(hipMemcpyAsync(h_tdt_ + 2 * cur, d_dt_, 2 * sizeof(double), hipMemcpyDeviceToHost, s_comp_));
+  HIP_CHECK(hipEventRecord(ev_tdt_[cur], s_comp_));
+  const bool have_prev = tdt_valid_;
+  tdt_valid_ = true;
+  if (have_prev) {
+    wait_event(ev_tdt_[cur ^ 1]);
+    const double dt = h_tdt_[2 * (cur ^ 1)], t = h_tdt_[2 * (cur ^ 1) + 1];  // d_dt_, d_time_ adjacent
+    if (t + 3.0 * dt < cfg_.t_end) return false;
+  }
+  return time() >= cfg_.t_end;
 }
 
 // ---- failure handling ------------------------------------------------------------------------------
@@ -1345,6 +1414,7 @@ void Solver::rollback() {
   HIP_CHECK(hipMemsetAsync(d_health_, 0, sizeof(unsigned), s_comp_));
   HIP_CHECK(hipStreamSynchronize(s_comp_));
   nstep_ = snap_step_;
+  tdt_valid_ = false;  // the lagged (dt, time) copy belongs to the discarded steps
   ++rollbacks_;
   cfg_.cfl *= cfg_.rollback_cfl_factor;  // captured as a kernel argument: re-capture the graphs
   invalidate_graphs();

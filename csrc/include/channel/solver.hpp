@@ -228,7 +228,13 @@ class Solver {
   std::thread ckpt_thread_;
   std::exception_ptr ckpt_error_;
   long ckpt_serial_ = 0;
-  unsigned long long run_nonce_ = 0;  // same on every rank of one run (from the communicator id): checkpoint markers  // P > 1: the first step runs eagerly (RCCL connection setup) before capture
+  unsigned long long run_nonce_ = 0;  // same on every rank of one run (from the communicator id): checkpoint markers
+  // t_end checks without a per-step host sync: (dt, time) of the last two steps in pinned memory
+  double* h_tdt_ = nullptr;
+  hipEvent_t ev_tdt_[2] = {nullptr, nullptr};
+  bool tdt_valid_ = false;
+  bool t_end_reached();
+  void wait_event(hipEvent_t e);      // event sync with the communicator watchdog (P > 1)
 
   // rollback snapshot
   void* snap_ = nullptr;

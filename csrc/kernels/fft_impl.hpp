@@ -364,7 +364,7 @@ constexpr int zphys_rows() {
 }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
-          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 1>
+          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 2>
 __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -383,19 +383,20 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   __shared__ T2 tws[TSA];  // twiddles staged once per block: LDS latency instead of L2 in the passes
   __shared__ float red[4][NWB];
   // lane: wave lane (reductions); t: thread within the row; w: row within the block
-  const int tid = threadIdx.x, lane = tid & 63, t = tid % TPR, w = tid / TPR;
+  const int tid = threadIdx.x, lane = tid & 63;
+  int t = tid % TPR, w = tid / TPR;
   for (int i = tid; i < TSA; i += ZWT * TPR) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;
   T2* frow = s + (tid / TPRF) * RWW * PITCH;  // first row of this thread's transform group
-  const int ft = tid % TPRF;
+  int ft = tid % TPRF;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
-  const long long r = static_cast<long long>(blockIdx.x) * ZWT + w;
+  const long long ngroups = (nrows + ZWT - 1) / ZWT;
   const int Kz = a.nkz - 1, nkz = a.nkz;
   const long long fs = a.field_stride;
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
   // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz)
-  auto zaddr = [&](int k) -> long long {
+  auto zaddr = [&](long long r, int k) -> long long {
     if constexpr (SEG) {
       const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
       return sp.off + r * sp.count + (k - sp.start);
@@ -403,31 +404,54 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       return r * nkz + k;
     }
   };
-
-  // (a persistent variant looping over row groups made the compiler hold ~380 registers: one wave
-  // per SIMD, 49.8 vs 44.3 ms/step).  Rows past the end (TPR < 64 only: the host checks
-  // nrows % ZWT == 0 otherwise) run the transforms on zeros and skip every global access.
-  const bool rv = r < nrows;
-  {
-    T2 ph[3][EP];
-    constexpr int MK = (NZP / 2 + TPR - 1) / TPR;
-    auto fetch = [&](int p, T2 (&va)[MK], T2 (&vb)[MK]) {
-      const T2* A = fields + (2 * p) * fs;
-      const T2* B = fields + (2 * p + 1) * fs;
+  // retained kz per thread: nkz = Nzp/3 + 1 (2/3 rule; checked on the host)
+  constexpr int MK = (NZP / 3 + 1 + TPR - 1) / TPR;
+  auto fetch = [&](long long r, int p, T2 (&va)[MK], T2 (&vb)[MK]) {
+    const bool rv = TPR < 64 ? r < nrows : true;
+    const T2* A = fields + (2 * p) * fs;
+    const T2* B = fields + (2 * p + 1) * fs;
 #pragma unroll
-      for (int i = 0; i < MK; ++i) {
-        const int k = t + TPR * i;
-        const bool ld = k < nkz && rv;
-        const long long o = ld ? zaddr(k) : 0;
-        va[i] = ld ? A[o] : T2{0, 0};
-        vb[i] = ld ? B[o] : T2{0, 0};
-      }
-    };
-    // the next pair's loads are in flight during each transform where the 24 registers fit (fp32,
-    // <= 1024 points, one segment); elsewhere each pair is loaded right before its transform
-    constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
-    T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
-    if constexpr (kPrefetch) fetch(0, pa, pb);
+    for (int i = 0; i < MK; ++i) {
+      const int k = t + TPR * i;
+      const bool ld = k < nkz && rv;
+      const long long o = ld ? zaddr(r, k) : 0;
+      va[i] = ld ? A[o] : T2{0, 0};
+      vb[i] = ld ? B[o] : T2{0, 0};
+    }
+  };
+  // The next pair's loads are in flight during each transform where the registers fit (fp32,
+  // <= 1024 points, one segment); elsewhere each pair is loaded right before its transform.
+  // Persistent launch (grid = resident capacity, the block walks row groups g, g + G, ...): the
+  // NEXT row's first pair is loaded during this row's forward transforms, so no row starts on an
+  // exposed load latency (the one-shot launch exposed it once per row: with the
+  // transforms skipped the stage still took 55 of its 88 us per 8-plane chunk).
+  constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
+  T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
+  long long g = blockIdx.x;
+  if constexpr (kPrefetch) {
+    if (g < ngroups) fetch(g * ZWT + w, 0, pa, pb);
+  }
+  // Rows past the end (TPR < 64 only: the host checks nrows % ZWT == 0 otherwise) run the
+  // transforms on zeros and skip every global access.  The loop is block-uniform.
+  for (; g < ngroups; g += gridDim.x) {
+    {
+      // the thread's lane-dependent addresses are re-derived per row from an opaque copy of the
+      // thread id: hoisted out of the row loop, the LDS and global address offsets of every pass
+      // stayed live across it (256 VGPRs + 74 spilled instead of 224 without the loop)
+      int tl = threadIdx.x;
+      asm volatile("" : "+v"(tl));
+      t = tl % TPR;
+      w = tl / TPR;
+      ft = tl % TPRF;
+      row = s + w * PITCH;
+      frow = s + (tl / TPRF) * RWW * PITCH;
+    }
+    const T2* twl = tws;
+    const long long r = g * ZWT + w;
+    const bool rv = TPR < 64 ? r < nrows : true;  // (TPR >= 64: the host checks nrows % ZWT == 0)
+    const long long rnext = (g + gridDim.x) * ZWT + w;
+    const bool more = g + gridDim.x < ngroups;
+    T2 ph[3][EP];
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       T2 va[MK], vb[MK];
@@ -438,16 +462,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           vb[i] = pb[i];
         }
       } else {
-        const T2* A = fields + (2 * p) * fs;
-        const T2* B = fields + (2 * p + 1) * fs;
-#pragma unroll
-        for (int i = 0; i < MK; ++i) {
-          const int k = t + TPR * i;
-          const bool ld = k < nkz && rv;
-          const long long o = ld ? zaddr(k) : 0;
-          va[i] = ld ? A[o] : T2{0, 0};
-          vb[i] = ld ? B[o] : T2{0, 0};
-        }
+        fetch(r, p, va, vb);
       }
       // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
       // (a real z-row has a real mean), zero padding between Kz and N-Kz.
@@ -465,10 +480,10 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       }
       for (int k = Kz + 1 + t; k < NZP - Kz; k += TPR) row[fft_pidx(k)] = T2{0, 0};
       if constexpr (kPrefetch) {
-        if (p < 2) fetch(p + 1, pa, pb);
+        if (p < 2) fetch(r, p + 1, pa, pb);
       }
       row_sync<TPRF>();
-      if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, true, TPRF>(frow, tws, ft);
+      if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, true, TPRF>(frow, twl, ft);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
         const int n = t + TPR * i;
@@ -495,12 +510,12 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
     }
     row_sync<TPRF>();
     const T sc = static_cast<T>(0.5 * a.scale);
-    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, twl, ft);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     // (unrolled: all LDS reads are issued before the global stores)
-    constexpr int MKO = (NZP / 2 + TPR - 1) / TPR;
+    constexpr int MKO = MK;  // retained kz per thread (nkz <= NZP/3 + 1)
     {
-      T2 z0[MKO], z1[MKO];
+      T2 z0[MKO] = {}, z1[MKO] = {};  // (zero-initialised: conditionally set arrays became loop-carried)
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
@@ -514,11 +529,16 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
         const int k = t + TPR * i;
         if (k < nkz && rv) {
           const T2 Z = z0[i], Zm = z1[i];
-          const long long o = zaddr(k);
+          const long long o = zaddr(r, k);
           fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
           fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
         }
       }
+    }
+    // the next row's first pair: in flight during this row's H_z transform and stores (and the
+    // next row's start); issued here, after the Hx/Hy stores, it adds nothing to the register peak
+    if constexpr (kPrefetch) {
+      if (more) fetch(rnext, 0, pa, pb);
     }
     row_sync<TPRF>();
     if constexpr (kHalf) {
@@ -531,9 +551,9 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
         if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
       }
       row_sync<TPRF>();
-      const T2* htw = tws + TS;
+      const T2* htw = twl + TS;
       if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPRF>(row, htw, ft);
-      T2 z0[MKO], z1[MKO], wk[MKO];
+      T2 z0[MKO] = {}, z1[MKO] = {}, wk[MKO] = {};
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
@@ -551,7 +571,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
           const T2 O2{z0[i].y + z1[i].y, z1[i].x - z0[i].x};
           const T2 X = cadd(E2, cmul_tw<false>(O2, wk[i]));
-          fields[2 * fs + zaddr(k)] = T2{X.x * sc, X.y * sc};
+          fields[2 * fs + zaddr(r, k)] = T2{X.x * sc, X.y * sc};
         }
       }
     } else {
@@ -561,9 +581,9 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       if (n < NZP) row[fft_pidx(n)] = T2{hz[i], T(0)};
     }
     row_sync<TPRF>();
-    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, tws, ft);
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, twl, ft);
     {
-      T2 z0[MKO], z1[MKO];
+      T2 z0[MKO] = {}, z1[MKO] = {};
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
@@ -575,10 +595,11 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
-        if (k < nkz && rv) fields[2 * fs + zaddr(k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
+        if (k < nkz && rv) fields[2 * fs + zaddr(r, k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
       }
     }
     }
+    row_sync<TPRF>();  // this row's last LDS reads precede the next row's writes
   }
   // block maxima -> one atomicMax per block and quantity
   for (int o = 32; o >= 1; o >>= 1) {
@@ -852,14 +873,26 @@ inline bool zhalf_enabled() {
   return on;
 }
 
-template <int NN, typename T, int TPR, int WPE = 1>
+// CHANNEL_ZPERS=0: one-shot z-stage grid (one row group per block) instead of the persistent one (A/B)
+inline bool zpers_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_ZPERS");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <int NN, typename T, int TPR, int WPE = 2>
 static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s, bool zh) {
   using T2 = typename C2<T>::type;
   constexpr int ZR = zphys_rows<NN, T, TPR>();
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
                          : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
-  dim3 grid(static_cast<unsigned>((nrows + ZR - 1) / ZR));
+  const long long ngroups = (nrows + ZR - 1) / ZR;
+  const long long cap = zpers_enabled() ? resident_blocks(reinterpret_cast<const void*>(kern), ZR * TPR) : ngroups;
+  dim3 grid(static_cast<unsigned>(std::min(ngroups, cap)));
+  CH_CHECK(a.nkz <= NN / 3 + 1, "zphys: more retained kz than the 2/3 rule allows");
   CH_CHECK(TPR < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
   hipLaunchKernelGGL(kern, grid, dim3(ZR * TPR), 0, s, a, static_cast<T2*>(fields), static_cast<const T2*>(tw.buf));
 }

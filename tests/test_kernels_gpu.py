@@ -99,9 +99,13 @@ def test_xfft(native, NX, nkz, dtype):
                                           (8, 384, torch.complex64), (4, 768, torch.complex64),
                                           (4, 768, torch.complex128), (2, 1536, torch.complex64),
                                           (4, 1536, torch.complex128), (4, 1280, torch.complex64),
-                                          (8, 160, torch.complex128)])
+                                          (8, 160, torch.complex128),
+                                          (1024, 1024, torch.complex64), (1024, 1024, torch.complex128),
+                                          (512, 2048, torch.complex64)])
 def test_zphys(native, NX, Nzp, dtype):
-    """z stage vs NumPy (LDS-pass kernel; the register-resident one is covered in a subprocess)."""
+    """z stage vs NumPy (LDS-pass kernel; the register-resident one is covered in a subprocess).
+    The 1024- and 2048-point cases have more row groups than the persistent grid holds, so blocks
+    walk several groups and the next row's first field pair is prefetched across rows."""
     rng = np.random.default_rng(Nzp)
     nkz = Nzp // 3 + 1
     ny = 3

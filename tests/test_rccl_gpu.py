@@ -110,7 +110,13 @@ def test_rccl_statistics_and_health(native):
     """Statistics step: plane sums go through the RCCL sum allreduce, health through the max."""
     ref = _run(native, b"", stats=True)
     got = _run(native, native.new_unique_id(), stats=True)
-    assert np.allclose(got[5], ref[5], rtol=1e-13, atol=0) and np.abs(got[5]).max() > 0
+    # per-line contributions are accumulated with device atomics (order-dependent rounding): compare
+    # against the scale of each statistic, not element by element (the Reynolds-stress row crosses 0)
+    N = len(got[5]) // 4
+    for q in range(4):
+        g, r = got[5][q * N:(q + 1) * N], ref[5][q * N:(q + 1) * N]
+        assert np.abs(g - r).max() <= 1e-13 * np.abs(r).max(), q
+    assert np.abs(got[5]).max() > 0
     assert got[0].health() == 0
     got[0].barrier()
 

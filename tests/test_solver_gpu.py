@@ -160,13 +160,20 @@ def test_turbulent_smoke_128(native, tmp_path):
 
 
 def test_t_end_stops_run(native):
-    """run() stops at the first step whose end time reaches t_end (device time read after a sync)."""
+    """run() stops at the first step whose end time reaches t_end.  Far from t_end the decision reads
+    the previous step's (dt, time) from pinned memory (no per-step host sync); near it, the device
+    time after a sync.  A second run() continues to a later t_end the same way."""
     s = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="random", stats_every=0,
                     log_every=0, symmetry_every=0, dt_fixed=0.01, t_end=0.055)
     s.init_ic()
     s.run(100, False)
     assert s.steps_done() == 6
     assert abs(s.time() - 0.06) < 1e-12
+    s2 = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="random", stats_every=0,
+                     log_every=0, symmetry_every=0, dt_fixed=0.01, t_end=0.405)
+    s2.init_ic()
+    s2.run(100, False)
+    assert s2.steps_done() == 41 and abs(s2.time() - 0.41) < 1e-12
 
 
 def test_phase_times_add_up(native):

@@ -13,6 +13,8 @@
 #   configs          bench.py on every BASELINE config that fits one GPU
 #   rehearse2        2-rank torchrun bench on one GPU over the shared-memory loopback data plane
 #   ab               bench.py once per env setting in AB_ENVS ("A=1 B=2;A=2 B=2")
+#   probe            transform stage alone (tools/xform_probe.py $PROBE_ARGS) per env setting in PROBE_ENVS
+#   kprobe           rocprofv3 kernel stats of the transform stage on one stream (env: $KPROBE_ENV)
 #   turb             long Re_tau~180 run (tools/turbulence.py $TURB_ARGS)
 # Output: gpurun_out/<TAG>_<step>.log (+ rocprofv3 directories).
 set -o pipefail
@@ -85,6 +87,42 @@ for step in "$@"; do
           || fail "ab [$envs]" gpurun_out/${tag}_ab$i.log
         echo "[$envs] $(tail -n 1 gpurun_out/${tag}_ab$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],3), "ms/step")')"
       done ;;
+    probe)
+      # transform stage alone, once per env setting in PROBE_ENVS ("A=1;A=2 B=3"); "-" = defaults
+      IFS=';' read -ra settings <<< "${PROBE_ENVS:--}"
+      : > $log
+      for envs in "${settings[@]}"; do
+        [ "$envs" = "-" ] && envs=""
+        env $envs timeout -k 10 200 python tools/xform_probe.py $PROBE_ARGS >> $log 2>&1 \
+          || fail "probe [$envs]" $log
+      done
+      cat $log ;;
+    kprobe)
+      # isolated kernel times of the transform stage (one stream) under a rocprofv3 kernel trace
+      env CHANNEL_YSTREAMS=1 $KPROBE_ENV timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_kprobe -o run \
+        --output-format csv -- python3 tools/xform_probe.py --reps 5 $PROBE_ARGS > $log 2>&1 || fail kprobe $log
+      python3 tools/kstats.py "$(find gpurun_out/${tag}_kprobe -name '*kernel_stats.csv' | head -n 1)" 10 ;;
+    pmcprobe)
+      # PMC passes over the transform stage alone (one stream): issue/latency/LDS/TA/TLB/MALL groups
+      i=0
+      for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+                 "SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL GRBM_GUI_ACTIVE" \
+                 "FETCH_SIZE TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum" \
+                 "WRITE_SIZE TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TD_TD_BUSY_sum TD_TC_STALL_sum" \
+                 ${PMC_EXTRA:+"$PMC_EXTRA"}; do
+        i=$((i + 1))
+        env CHANNEL_YSTREAMS=1 $KPROBE_ENV timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d gpurun_out/${tag}_pmcp$i \
+          -o run --output-format csv -- python3 ${PMC_PROG:-tools/xform_probe.py --reps 2 --warmup 1 $PROBE_ARGS} \
+          > gpurun_out/${tag}_pmcp$i.log 2>&1
+        st=$?
+        if [ $st -ne 0 ]; then
+          echo "pmc pass $i [$grp] exit $st"; tail -n 5 gpurun_out/${tag}_pmcp$i.log
+          case $st in 124|134|137|139) exit 1 ;; esac
+        fi
+      done
+      python3 tools/pmc_summary.py gpurun_out/${tag}_pmcp* > $log 2>&1 || fail pmc_summary $log
+      echo "pmcprobe: $i passes -> $log" ;;
     turb)
       timeout -k 10 ${TURB_TL:-1000} python -u tools/turbulence.py $TURB_ARGS > $log 2>&1 || fail turb $log
       tail -n 5 $log ;;
