@@ -113,6 +113,24 @@ void RcclComm::alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) 
   NCCL_CHECK(ncclGroupEnd());
 }
 
+std::unique_ptr<Comm> RcclComm::group(const std::vector<int>& members) {
+  auto c = static_cast<ncclComm_t>(comm_);
+  CH_CHECK(c, "RcclComm: communicator was aborted");
+  int key = -1;
+  for (size_t i = 0; i < members.size(); ++i)
+    if (members[i] == rank_) key = static_cast<int>(i);
+  CH_CHECK(key >= 0 && !members.empty(), "RcclComm::group: rank " << rank_ << " is not in its own group");
+  ncclComm_t sub = nullptr;
+  NCCL_CHECK(ncclCommSplit(c, members[0], key, &sub, nullptr));
+  std::unique_ptr<RcclComm> g(new RcclComm());
+  g->comm_ = sub;
+  NCCL_CHECK(ncclCommUserRank(sub, &g->rank_));
+  NCCL_CHECK(ncclCommCount(sub, &g->size_));
+  CH_CHECK(g->rank_ == key && g->size_ == static_cast<int>(members.size()), "ncclCommSplit: unexpected group layout");
+  g->self_via_rccl_ = self_via_rccl_;
+  return g;
+}
+
 void RcclComm::allreduce_max_f32(float* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclFloat, ncclMax, static_cast<ncclComm_t>(comm_), s));
 }
@@ -124,6 +142,68 @@ void RcclComm::allreduce_max_f64(double* buf, size_t n, hipStream_t s) {
 }
 void RcclComm::allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, static_cast<ncclComm_t>(comm_), s));
+}
+
+// ---- group view -------------------------------------------------------------------------------
+GroupComm::GroupComm(Comm* world, std::vector<int> members) : world_(world), members_(std::move(members)) {
+  size_ = static_cast<int>(members_.size());
+  rank_ = -1;
+  for (int i = 0; i < size_; ++i)
+    if (members_[i] == world_->rank()) rank_ = i;
+  CH_CHECK(rank_ >= 0, "GroupComm: rank " << world_->rank() << " is not in its own group");
+}
+
+void GroupComm::unsupported() { CH_CHECK(false, "reductions over an exchange group are not supported"); }
+
+A2ABlock GroupComm::widen(const A2ABlock& o) const {
+  CH_CHECK(o.scount.size() == static_cast<size_t>(size_) && o.rcount.size() == static_cast<size_t>(size_),
+           "alltoallv: count vectors must have one entry per group rank");
+  const size_t W = static_cast<size_t>(world_->size());
+  A2ABlock w;
+  w.send = o.send;
+  w.recv = o.recv;
+  w.scount.assign(W, 0);
+  w.soff.assign(W, 0);
+  w.rcount.assign(W, 0);
+  w.roff.assign(W, 0);
+  for (int i = 0; i < size_; ++i) {
+    const int g = members_[i];
+    w.scount[g] = o.scount[i];
+    w.soff[g] = o.soff[i];
+    w.rcount[g] = o.rcount[i];
+    w.roff[g] = o.roff[i];
+  }
+  return w;
+}
+
+void GroupComm::alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff,
+                          void* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& roff,
+                          hipStream_t s) {
+  A2ABlock b;
+  b.send = send;
+  b.recv = recv;
+  b.scount = scount;
+  b.soff = soff;
+  b.rcount = rcount;
+  b.roff = roff;
+  alltoallv_batch({b}, s);
+}
+
+void GroupComm::alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) {
+  std::vector<A2ABlock> w;
+  w.reserve(ops.size());
+  for (const auto& o : ops) w.push_back(widen(o));
+  world_->alltoallv_batch(w, s);
+}
+
+std::unique_ptr<Comm> GroupComm::group(const std::vector<int>& members) {
+  std::vector<int> m;
+  for (int i : members) m.push_back(members_.at(i));
+  return std::make_unique<GroupComm>(world_, m);
+}
+
+std::unique_ptr<Comm> ShmComm::group(const std::vector<int>& members) {
+  return std::make_unique<GroupComm>(this, members);
 }
 
 // ---- shared-memory loopback (tests) -----------------------------------------------------------

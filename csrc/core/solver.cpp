@@ -127,6 +127,14 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
     const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
     if (!comm_->graph_capturable() || (gm && std::atoi(gm) == 0)) use_graph_ = false;
     if (const char* t = std::getenv("CHANNEL_COMM_TIMEOUT_S")) comm_timeout_s_ = std::atof(t);
+    if (plan_.pencil()) {
+      // one communicator per decomposition axis (collective: same call order on every rank)
+      std::vector<int> col, row;
+      for (int c = 0; c < plan_.Pc; ++c) col.push_back(plan_.rank_of(plan_.prow, c));
+      for (int r = 0; r < plan_.Pr; ++r) row.push_back(plan_.rank_of(r, plan_.pcol));
+      comm_col_ = comm_->group(col);
+      comm_row_ = comm_->group(row);
+    }
   }
   ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
   tw_x_.build(plan_.NX, fp64_);
@@ -146,6 +154,8 @@ Solver::~Solver() {
   } catch (...) {
   }
   free_all();
+  comm_row_.reset();
+  comm_col_.reset();
   comm_.reset();
   if (s_comp_) (void)hipStreamDestroy(s_comp_);
   if (s_comm_) (void)hipStreamDestroy(s_comm_);
@@ -251,6 +261,10 @@ void Solver::free_all() {
   s_extra_.clear();
   for (auto* v : {&ev_cb_, &ev_cc_})
     for (auto e : *v) (void)hipEventDestroy(e);
+  for (auto& v : ev_pen_) {
+    for (auto e : v) (void)hipEventDestroy(e);
+    v.clear();
+  }
   for (auto& pr : step_ev_) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -698,6 +712,10 @@ void Solver::transforms(int n, bool /*stats*/) {
     transforms_slab(n, xa, za, da);
     return;
   }
+  if (std::getenv("CHANNEL_PENCIL_UNCHUNKED") == nullptr) {
+    transforms_pencil(n, xa, za, da);
+    return;
+  }
   // ---- pencil: per-field exchanges on the comm stream, overlapped with the x transforms ----
   const int Pc = p.Pc, Pr = p.Pr;
   const bool pen = p.pencil();
@@ -802,7 +820,8 @@ void Solver::transforms(int n, bool /*stats*/) {
   HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
 }
 
-// Exchange of y chunk k for the slab (Pr = 1): chunk k holds rows [k*ch, (k+1)*ch) of EVERY
+// Exchange of y chunk k over the column group (the slab: every rank; the pencil: the Pc ranks of
+// this process row, A exchange kx <-> y): chunk k holds rows [k*ch, (k+1)*ch) of EVERY
 // rank's y range, so the chunk count is the same on all ranks (uneven splits send empty blocks
 // at the end).  Backward (to_phys): my spectral rows Y_c[k] of fields 0..nf-1 go to rank c and
 // land in c's receive block [src][y_loc][nkx_src][kz] at row k*ch; forward: the transformed rows
@@ -811,7 +830,7 @@ void Solver::transforms(int n, bool /*stats*/) {
 // MPI_Alltoall, channel_cuda_mpi.c:64-128).
 void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
   const Plan& p = plan_;
-  const int P = p.P, lines = p.lines_loc();
+  const int P = p.Pc, lines = p.lines_loc();  // column group (slab: the world)
   const size_t nr_me = static_cast<size_t>(std::max(0, std::min(ch, p.ny_loc - k * ch)));
   std::vector<A2ABlock> ops(nf);
   for (int f = 0; f < nf; ++f) {
@@ -823,7 +842,7 @@ void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
     char* spec = static_cast<char*>(field_ptr(OUT0 + f));
     char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
     for (int c = 0; c < P; ++c) {
-      if (self_direct_ && c == p.rank) continue;  // read/written in place by the x transforms
+      if (self_direct_ && c == p.pcol) continue;  // read/written in place by the x transforms
       const size_t nr_c = static_cast<size_t>(std::max(0, std::min(ch, p.y_split.count[c] - k * ch)));
       const size_t yo = (static_cast<size_t>(p.y_split.start[c]) + static_cast<size_t>(k) * ch) * lines * esz_;
       const size_t yc = nr_c * lines * esz_;
@@ -845,7 +864,7 @@ void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
     o.send = to_phys ? static_cast<const void*>(spec) : static_cast<const void*>(xb);
     o.recv = to_phys ? static_cast<void*>(xb) : static_cast<void*>(spec);
   }
-  comm_->alltoallv_batch(ops, s_comm_);
+  col_comm()->alltoallv_batch(ops, s_comm_);
 }
 
 // P > 1 slab substep transforms, y-chunked and pipelined over two streams:
@@ -932,6 +951,187 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     ev(4, true, s_comm_);
   }
   if (n == 0) {  // every chunk's z stage precedes ev_cc_[nch-1], which the comm stream waited on
+    ev(5, false, s_comm_);
+    comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+    ev(5, true, s_comm_);
+  }
+  HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+  if (n == 0) dt_update(da, s_comp_);
+  roctxRangePop();
+}
+
+// B exchange of y chunk k over the row group (the Pr ranks of this process column, x <-> kz):
+// the x-expanded rows of the chunk, blocked by destination row r ([r][y_loc][x_r][kz_loc]), go to
+// row peer r and land in its z-row buffer [src][y_loc][x_loc][kz_src] at row k*ch (to_z), and the
+// z stage's H rows come back the same way (!to_z).  Every block is contiguous: no packing.
+void Solver::b2b_pencil_chunk(int k, int ch, bool to_z, int nf) {
+  const Plan& p = plan_;
+  const int Pr = p.Pr;
+  const size_t y0 = static_cast<size_t>(k) * ch;
+  const size_t nr = static_cast<size_t>(std::max(0, std::min(ch, p.ny_loc - k * ch)));
+  std::vector<A2ABlock> ops(nf);
+  for (int f = 0; f < nf; ++f) {
+    A2ABlock& o = ops[f];
+    o.scount.assign(Pr, 0);
+    o.soff.assign(Pr, 0);
+    o.rcount.assign(Pr, 0);
+    o.roff.assign(Pr, 0);
+    char* xe = static_cast<char*>(phys_) + static_cast<size_t>(f) * physn_ * esz_;
+    char* zr = static_cast<char*>(zbuf_) + static_cast<size_t>(f) * zstride_ * esz_;
+    for (int r = 0; r < Pr; ++r) {
+      const size_t xo = (static_cast<size_t>(p.ny_loc) * p.x_split.start[r] + y0 * p.x_split.count[r]) * p.nkz_loc * esz_;
+      const size_t xc = nr * p.x_split.count[r] * p.nkz_loc * esz_;
+      const size_t zo = (static_cast<size_t>(p.ny_loc) * p.nx_loc * p.kz_split.start[r] + y0 * p.nx_loc * p.kz_split.count[r]) * esz_;
+      const size_t zc = nr * p.nx_loc * p.kz_split.count[r] * esz_;
+      if (to_z) {
+        o.soff[r] = xc ? xo : 0;
+        o.scount[r] = xc;
+        o.roff[r] = zc ? zo : 0;
+        o.rcount[r] = zc;
+      } else {
+        o.soff[r] = zc ? zo : 0;
+        o.scount[r] = zc;
+        o.roff[r] = xc ? xo : 0;
+        o.rcount[r] = xc;
+      }
+    }
+    o.send = to_z ? static_cast<const void*>(xe) : static_cast<const void*>(zr);
+    o.recv = to_z ? static_cast<void*>(zr) : static_cast<void*>(xe);
+  }
+  comm_row_->alltoallv_batch(ops, s_comm_);
+}
+
+// P = Pr x Pc pencil substep transforms: the slab's y-chunked pipeline with the row-group B
+// exchange between the x transforms and the z stage, as a software pipeline over two streams.
+// Per chunk k the stages are A-in(k) -> x-backward(k) -> B-in(k) -> z(k) -> B-out(k) ->
+// x-forward(k) -> A-out(k); in issue step t the comm stream runs A-in(t), B-in(t-2), B-out(t-4),
+// A-out(t-6) and the compute stream x-backward(t-1), z(t-3), x-forward(t-5), each waiting only on
+// the event its predecessor recorded in step t-1.  Every exchange is one batched group on its
+// axis communicator (RCCL: ncclCommSplit), the chunk's intermediates are produced and consumed
+// back to back (Infinity Cache), and the whole schedule is captured in the step graph.  The
+// arithmetic is the unchunked sequence's (bitwise).
+void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const DtArgs& da) {
+  const Plan& p = plan_;
+  const int Pc = p.Pc, Pr = p.Pr;
+  const int maxrows = p.y_split.max_count();
+  const int ch = (ychunk_p_ > 0 && ychunk_p_ < maxrows) ? ychunk_p_ : maxrows;
+  const int nch = (maxrows + ch - 1) / ch;
+  for (auto& v : ev_pen_)
+    while (static_cast<int>(v.size()) < nch) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      v.push_back(e);
+    }
+  enum { E_A = 0, E_XB, E_B, E_Z, E_BF, E_XF };
+  XArgs xa = xa0;
+  xa.nkz = p.nkz_loc;
+  xa.field_stride_spec = static_cast<long long>(xstride_);
+  xa.npseg = Pr;
+  for (int r = 0; r < Pr; ++r) xa.x_start[r] = p.x_split.start[r];
+  xa.x_start[Pr] = p.NX;
+  XSrc src;
+  src.base = xbuf_;
+  src.nsrc = Pc;
+  XDst dst;
+  dst.base = xbuf_;
+  dst.ndst = Pc;
+  for (int c = 0; c < Pc; ++c) src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
+  src.kx_start[Pc] = dst.kx_start[Pc] = p.nkx;
+  if (self_direct_) {  // own column block: straight from / into the spectral fields
+    src.self_seg = dst.self_seg = p.pcol;
+    src.self_base = out_;
+    dst.self_base = out_;
+    src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
+    CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
+  }
+  ZArgs za = za0;
+  za.NX = p.nx_loc;
+  za.field_stride = static_cast<long long>(zstride_);
+  za.nseg = Pr;
+  for (int r = 0; r < Pr; ++r) za.kz_start[r] = p.kz_split.start[r];
+  za.kz_start[Pr] = p.nkz;
+  // chunk-dependent offsets
+  auto chunk_rows = [&](int k) { return std::max(0, std::min(ch, p.ny_loc - k * ch)); };
+  auto set_x = [&](int k, XArgs& x, XSrc& sc, XDst& dc) {
+    const long long y0 = static_cast<long long>(k) * ch;
+    x.ny = chunk_rows(k);
+    for (int r = 0; r < Pr; ++r)
+      x.poff[r] = (static_cast<long long>(p.ny_loc) * p.x_split.start[r] + y0 * p.x_split.count[r]) * p.nkz_loc;
+    for (int c = 0; c < Pc; ++c)
+      sc.off[c] = dc.off[c] = (static_cast<long long>(p.ny_loc) * p.kx_split.start[c] + y0 * p.kx_split.count[c]) * p.nkz_loc;
+    if (self_direct_) sc.off[p.pcol] = dc.off[p.pcol] = (static_cast<long long>(p.y0) + y0) * p.lines_loc();
+  };
+  auto xbw = [&](int k) {
+    if (chunk_rows(k) > 0) {
+      XArgs x = xa;
+      XSrc sc = src;
+      XDst dc = dst;
+      set_x(k, x, sc, dc);
+      x.nfields = 6;
+      ev(1, false);
+      xfft_backward(x, sc, phys_, tw_x_, fp64_, s_comp_);
+      ev(1, true);
+    }
+    HIP_CHECK(hipEventRecord(ev_pen_[E_XB][k], s_comp_));
+  };
+  auto zst = [&](int k) {
+    if (chunk_rows(k) > 0) {
+      ZArgs z = za;
+      const long long y0 = static_cast<long long>(k) * ch;
+      z.ny = chunk_rows(k);
+      z.y0 = p.y0 + static_cast<int>(y0);
+      for (int r = 0; r < Pr; ++r)
+        z.off[r] = static_cast<long long>(p.ny_loc) * p.nx_loc * p.kz_split.start[r] + y0 * p.nx_loc * p.kz_split.count[r];
+      ev(2, false);
+      zphys(z, zbuf_, tw_z_, fp64_, s_comp_);
+      ev(2, true);
+    }
+    HIP_CHECK(hipEventRecord(ev_pen_[E_Z][k], s_comp_));
+  };
+  auto xfw = [&](int k) {
+    if (chunk_rows(k) > 0) {
+      XArgs x = xa;
+      XSrc sc = src;
+      XDst dc = dst;
+      set_x(k, x, sc, dc);
+      x.nfields = 3;
+      ev(3, false);
+      xfft_forward(x, phys_, dc, tw_x_, fp64_, s_comp_);
+      ev(3, true);
+    }
+    HIP_CHECK(hipEventRecord(ev_pen_[E_XF][k], s_comp_));
+  };
+  auto comm_op = [&](int k, int wait_ev, int rec_ev, const std::function<void()>& f) {
+    if (wait_ev >= 0) HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_pen_[wait_ev][k], 0));
+    ev(4, false, s_comm_);
+    f();
+    ev(4, true, s_comm_);
+    if (rec_ev >= 0) HIP_CHECK(hipEventRecord(ev_pen_[rec_ev][k], s_comm_));
+  };
+
+  roctxRangePushA("xzx_pencil_chunked");
+  HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  for (int t = 0; t < nch + 6; ++t) {
+    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_chunk(t, ch, true, 6); });
+    if (t - 2 >= 0 && t - 2 < nch) comm_op(t - 2, E_XB, E_B, [&] { b2b_pencil_chunk(t - 2, ch, true, 6); });
+    if (t - 4 >= 0 && t - 4 < nch) comm_op(t - 4, E_Z, E_BF, [&] { b2b_pencil_chunk(t - 4, ch, false, 3); });
+    if (t - 6 >= 0 && t - 6 < nch) comm_op(t - 6, E_XF, -1, [&] { a2a_slab_chunk(t - 6, ch, false, 3); });
+    if (t - 1 >= 0 && t - 1 < nch) {
+      HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_pen_[E_A][t - 1], 0));
+      xbw(t - 1);
+    }
+    if (t - 3 >= 0 && t - 3 < nch) {
+      HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_pen_[E_B][t - 3], 0));
+      zst(t - 3);
+    }
+    if (t - 5 >= 0 && t - 5 < nch) {
+      HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_pen_[E_BF][t - 5], 0));
+      xfw(t - 5);
+    }
+  }
+  if (n == 0) {  // every z stage precedes the last A-out on the comm stream (E_Z -> E_BF -> E_XF)
     ev(5, false, s_comm_);
     comm_->allreduce_max_f32(d_max_, 4, s_comm_);
     ev(5, true, s_comm_);
@@ -1055,7 +1255,7 @@ void Solver::wait(hipStream_t s) {
     const hipError_t e = hipStreamQuery(s);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) HIP_CHECK(e);
-    if (comm_->async_error()) {
+    if (comm_failed()) {
       comm_->abort();
       CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
     }
@@ -1068,6 +1268,10 @@ void Solver::wait(hipStream_t s) {
   }
 }
 
+bool Solver::comm_failed() {
+  return comm_->async_error() || (comm_col_ && comm_col_->async_error()) || (comm_row_ && comm_row_->async_error());
+}
+
 void Solver::wait_event(hipEvent_t e) {
   if (!comm_) {
     HIP_CHECK(hipEventSynchronize(e));
@@ -1078,7 +1282,7 @@ void Solver::wait_event(hipEvent_t e) {
     const hipError_t r = hipEventQuery(e);
     if (r == hipSuccess) return;
     if (r != hipErrorNotReady) HIP_CHECK(r);
-    if (comm_->async_error()) {
+    if (comm_failed()) {
       comm_->abort();
       CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
     }

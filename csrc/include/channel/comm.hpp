@@ -51,6 +51,13 @@ class Comm {
   // asynchronous communicator failure (peer died, network error); polled by the solver's watchdog
   virtual bool async_error() { return false; }
 
+  // Sub-communicator of one exchange group (collective over this communicator: every rank calls it
+  // with the member list of its own group; groups partition the ranks).  members[i] is the rank in
+  // this communicator of group rank i.  RCCL: ncclCommSplit (color = members[0], key = position);
+  // the host-staged loopback: a view that widens group counts to the world (every rank of the world
+  // still enters each exchange, as the solver's schedule is identical on all ranks).
+  virtual std::unique_ptr<Comm> group(const std::vector<int>& members) = 0;
+
   static std::string new_unique_id();  // 128 raw bytes (RCCL)
   // "shm:<name>" -> ShmComm, otherwise an RCCL unique id
   static std::unique_ptr<Comm> create(int rank, int nranks, const std::string& uid, int device);
@@ -74,8 +81,10 @@ class RcclComm final : public Comm {
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
   void abort() override;
   bool async_error() override;
+  std::unique_ptr<Comm> group(const std::vector<int>& members) override;
 
  private:
+  RcclComm() = default;
   void* comm_ = nullptr;  // ncclComm_t
   // the block a rank sends to itself is a D2D copy on the stream; CHANNEL_A2A_SELF=rccl routes it
   // through ncclSend/ncclRecv instead (lets a 1-rank communicator exercise RCCL's point-to-point path)
@@ -96,6 +105,7 @@ class ShmComm final : public Comm {
   void allreduce_max_u32(unsigned* buf, size_t n, hipStream_t s) override;
   void abort() override { failed_ = true; }
   bool async_error() override { return failed_; }
+  std::unique_ptr<Comm> group(const std::vector<int>& members) override;
 
  private:
   void barrier();
@@ -107,6 +117,31 @@ class ShmComm final : public Comm {
   std::string name_;
   void* base_ = nullptr;
   size_t bytes_ = 0, slot_bytes_ = 0;
+};
+
+// Group view on a world communicator (exchange counts widened with zeros outside the group).
+class GroupComm final : public Comm {
+ public:
+  GroupComm(Comm* world, std::vector<int> members);
+  bool graph_capturable() const override { return world_->graph_capturable(); }
+  const char* kind() const override { return world_->kind(); }
+  void alltoallv(const void* send, const std::vector<size_t>& scount, const std::vector<size_t>& soff, void* recv,
+                 const std::vector<size_t>& rcount, const std::vector<size_t>& roff, hipStream_t s) override;
+  void alltoallv_batch(const std::vector<A2ABlock>& ops, hipStream_t s) override;
+  // reductions stay on the world communicator (the solver never reduces over a group)
+  void allreduce_max_f32(float*, size_t, hipStream_t) override { unsupported(); }
+  void allreduce_sum_f64(double*, size_t, hipStream_t) override { unsupported(); }
+  void allreduce_max_f64(double*, size_t, hipStream_t) override { unsupported(); }
+  void allreduce_max_u32(unsigned*, size_t, hipStream_t) override { unsupported(); }
+  void abort() override { world_->abort(); }
+  bool async_error() override { return world_->async_error(); }
+  std::unique_ptr<Comm> group(const std::vector<int>&) override;
+
+ private:
+  [[noreturn]] static void unsupported();
+  A2ABlock widen(const A2ABlock& o) const;
+  Comm* world_;
+  std::vector<int> members_;
 };
 
 }  // namespace channel

@@ -465,6 +465,59 @@ __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restr
   if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV, TPR>(buf, tw + Pl::T1, lane);
 }
 
+// ---- register-edge passes (one butterfly column per lane: N / R0 == TPR) ------------------------
+// When the first pass has exactly one butterfly per lane (Q = N/R0 = TPR), lane j's inputs are the
+// elements j + r Q, which is the "point n = lane + TPR i" register layout the z stage keeps its
+// physical rows in; and when the last pass has NS = N/R a multiple of TPR, its outputs j + r NS
+// (j = lane + TPR b) are that layout again.  So a transform can start from and end in registers,
+// saving the gather-to-LDS and the read-back round trips of the LDS-only version.
+template <int N>
+struct FftLast {  // radix and stride of the last pass
+  static constexpr int R = FftPlan<N>::R2 > 1 ? FftPlan<N>::R2 : FftPlan<N>::R1;
+  static constexpr int NS = N / R;
+  static constexpr int TOFF = FftPlan<N>::R2 > 1 ? FftPlan<N>::T1 : 0;  // its twiddle table
+};
+template <int N, int TPR>
+constexpr bool fft_reg_edges_ok() {
+  return FftPlan<N>::R0 * TPR == N && FftPlan<N>::R1 > 1 && FftLast<N>::NS % TPR == 0;
+}
+// first pass (NS = 1) from registers: x[r] = element j + r N/R0 (j = lane); writes its output
+template <int N, bool INV, typename T2>
+__device__ __forceinline__ void wave_pass_first_reg(T2* __restrict__ buf, T2 (&x)[FftPlan<N>::R0], int j) {
+  constexpr int R = FftPlan<N>::R0;
+  dftR<R, INV>(x);
+#pragma unroll
+  for (int r = 0; r < R; ++r) buf[fft_pidx(j * R + r)] = x[r];
+}
+// middle pass (the second of a three-pass plan) through LDS
+template <int N, int PITCH, bool INV, int TPR, typename T2>
+__device__ __forceinline__ void wave_pass_middle(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
+  using Pl = FftPlan<N>;
+  static_assert(Pl::R2 > 1, "middle pass of a three-pass plan");
+  wave_pass<N, Pl::R1, Pl::R0, 1, PITCH, INV, TPR>(buf, tw, lane);
+}
+// last pass into registers: out[b + r B] = element j + r NS, j = lane + TPR b, B = NS / TPR
+template <int N, bool INV, int TPR, typename T2>
+__device__ __forceinline__ void wave_pass_last_reg(const T2* __restrict__ buf, const T2* __restrict__ tw,
+                                                   T2 (&out)[N / TPR], int lane) {
+  constexpr int R = FftLast<N>::R, NS = FftLast<N>::NS, B = NS / TPR;
+  const T2* t = tw + FftLast<N>::TOFF;
+  T2 v[B][R];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[b][r] = buf[fft_pidx(lane + TPR * b + r * NS)];
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    const int j = lane + TPR * b;
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[b][r] = cmul_tw<INV>(v[b][r], t[(r - 1) * NS + j]);
+    dftR<R, INV>(v[b]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[b + r * B] = v[b][r];
+  }
+}
+
 // length-N/2 transform of HalfPlan<N>; htw points at the appended tables (post twiddles first)
 template <int N, int PITCH, bool INV, int TPR = 64, typename T2>
 __device__ __forceinline__ void wave_fft_half(T2* __restrict__ buf, const T2* __restrict__ htw, int lane) {

@@ -148,8 +148,15 @@ class Solver {
   hipEvent_t timing_event();
   // P > 1 slab: y-chunked backward exchange -> x -> z -> x -> forward exchange pipeline
   void transforms_slab(int n, const XArgs& xa, const ZArgs& za, const DtArgs& da);
-  // exchange of y chunk k (rows [k*ch, (k+1)*ch) of every rank's y range) for nf fields
+  // exchange of y chunk k (rows [k*ch, (k+1)*ch) of every rank's y range) for nf fields over the
+  // column group (the world for the slab)
   void a2a_slab_chunk(int k, int ch, bool to_phys, int nf);
+  // pencil: the same y-chunked pipeline with the B exchange (row group, x <-> kz) between the x
+  // transforms and the z stage
+  void transforms_pencil(int n, const XArgs& xa, const ZArgs& za, const DtArgs& da);
+  void b2b_pencil_chunk(int k, int ch, bool to_z, int nf);
+  Comm* col_comm() const { return comm_col_ ? comm_col_.get() : comm_.get(); }
+  bool comm_failed();
   void write_logs(const StepLog& L, bool verbose);
   void write_stats_files(const std::vector<double>& st);
   void write_spectra_files(const Spectra& sp);
@@ -176,6 +183,9 @@ class Solver {
   size_t esz_ = 8;  // bytes per complex element
   hipStream_t s_comp_ = nullptr, s_comm_ = nullptr;
   std::unique_ptr<Comm> comm_;
+  // pencil exchange groups (one communicator per decomposition axis): column group
+  // (same process row, Pc ranks: A exchange kx <-> y) and row group (same column, Pr ranks: B)
+  std::unique_ptr<Comm> comm_col_, comm_row_;
   YTablesDev ytab_;
   Twiddles tw_x_, tw_z_;
 
@@ -208,6 +218,8 @@ class Solver {
   std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
   std::vector<hipEvent_t> ev_cb_, ev_cc_;  // per y-chunk: backward exchange done, compute done
+  // pencil pipeline, per y chunk: A in, x-backward, B in, z stage, B out, x-forward done
+  std::vector<hipEvent_t> ev_pen_[6];
   int ychunk_p_ = 0;                       // y planes per chunk of the P > 1 slab pipeline
   bool self_direct_ = true;                // slab: own kx block read/written in place (no self copy)
   // phase timing: event pool and the (phase, start, end) pairs of the current step

@@ -426,6 +426,10 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   // exposed load latency (the one-shot launch exposed it once per row: with the
   // transforms skipped the stage still took 55 of its 88 us per 8-plane chunk).
   constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
+  // register-edge transforms (first pass from and last pass into registers, fft_device.hpp) where
+  // one wave owns a row and the plan has one first-pass butterfly per lane (NZP = 1024: 16x16x4)
+  constexpr bool kRegEdge = TPR == 64 && EP == 16 && FftPlan<NZP>::R0 == 16 && FftPlan<NZP>::R2 > 1 &&
+                            fft_reg_edges_ok<NZP, 64>() && 2 * MK <= 16;
   T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
   long long g = blockIdx.x;
   if constexpr (kPrefetch) {
@@ -466,6 +470,47 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       }
       // Z_k = A_k + i B_k, Z_{N-k} = conj(A_k) + i conj(B_k); the kz=0 imaginary parts are dropped
       // (a real z-row has a real mean), zero padding between Kz and N-Kz.
+      if constexpr (kRegEdge) {
+        // First pass straight from the loaded registers: lane t's butterfly takes Z at t + 64 r,
+        // r < MK directly (the lane's own modes) and, for r >= 16 - MK, the mirror Z_{N-k} of mode
+        // k = 64 (15 - r) + (64 - t) held by lane 64 - t (lane 0: its own mode 64 (16 - r)); the
+        // band between is the zero padding.  The mirror values cross lanes by ds_bpermute, 2
+        // dwords per slot, instead of a row gather through LDS.
+        T2 d[MK], m[MK];
+#pragma unroll
+        for (int i = 0; i < MK; ++i) {
+          const int k = t + TPR * i;
+          const bool ok = k < nkz;
+          d[i] = ok ? (k == 0 ? T2{va[i].x, vb[i].x} : T2{va[i].x - vb[i].y, va[i].y + vb[i].x}) : T2{0, 0};
+          m[i] = ok && k > 0 ? T2{va[i].x + vb[i].y, vb[i].x - va[i].y} : T2{0, 0};
+        }
+        if constexpr (kPrefetch) {
+          if (p < 2) fetch(r, p + 1, pa, pb);
+        }
+        const int src = (64 - t) & 63;
+        T2 x[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          if (q < MK) {
+            x[q] = d[q];
+          } else if (q < 16 - MK) {
+            x[q] = T2{0, 0};
+          } else {
+            const T2 pm{__shfl(m[15 - q].x, src), __shfl(m[15 - q].y, src)};
+            x[q] = t != 0 ? pm : (16 - q < MK ? m[16 - q] : T2{0, 0});
+          }
+        }
+        if (!(a.diag & 1)) {
+          wave_pass_first_reg<NZP, true>(row, x, t);
+          row_sync<64>();
+          wave_pass_middle<NZP, PITCH, true, 64>(row, twl, t);
+          wave_pass_last_reg<NZP, true, 64>(row, twl, ph[p], t);
+        } else {
+#pragma unroll
+          for (int i = 0; i < EP; ++i) ph[p][i] = x[i];
+        }
+        row_sync<64>();  // the last pass's reads precede the next pair's first-pass writes
+      } else {
 #pragma unroll
       for (int i = 0; i < MK; ++i) {
         const int k = t + TPR * i;
@@ -490,11 +535,13 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
         ph[p][i] = n < NZP ? row[fft_pidx(n)] : T2{0, 0};
       }
       row_sync<TPRF>();
+      }
     }
     // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
     const int yl = rv ? static_cast<int>(r / a.NX) : 0;
     const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
     T hz[EP];
+    T2 hxy[kRegEdge ? EP : 1];
 #pragma unroll
     for (int i = 0; i < EP; ++i) {
       const T u = ph[0][i].x, v = ph[0][i].y, ww = ph[1][i].x, wx = ph[1][i].y, wy = ph[2][i].x, wz = ph[2][i].y;
@@ -506,14 +553,42 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       mw = fmaxf(mw, aw);
       mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
       const int n = t + TPR * i;
-      if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
+      if constexpr (kRegEdge) hxy[i] = T2{hx, hy};
+      else if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
     }
-    row_sync<TPRF>();
     const T sc = static_cast<T>(0.5 * a.scale);
-    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, twl, ft);
     // (Hx + i Hy)^_k = Z_k: Hx_k = (Z_k + conj Z_{N-k})/2, Hy_k = (Z_k - conj Z_{N-k})/(2i)
     // (unrolled: all LDS reads are issued before the global stores)
     constexpr int MKO = MK;  // retained kz per thread (nkz <= NZP/3 + 1)
+    if constexpr (kRegEdge) {
+      // first pass from the product registers, last pass into registers; Z_{N-k} of the lane's
+      // mode k = t + 64 i sits in lane 64 - t at slot 15 - i (lane 0: its own slot 16 - i)
+      T2 z[EP];
+      if (!(a.diag & 1)) {
+        wave_pass_first_reg<NZP, false>(row, hxy, t);
+        row_sync<64>();
+        wave_pass_middle<NZP, PITCH, false, 64>(row, twl, t);
+        wave_pass_last_reg<NZP, false, 64>(row, twl, z, t);
+      } else {
+#pragma unroll
+        for (int i = 0; i < EP; ++i) z[i] = hxy[i];
+      }
+      const int src = (64 - t) & 63;
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        const T2 pm{__shfl(z[15 - i].x, src), __shfl(z[15 - i].y, src)};
+        const T2 Zm = t != 0 ? pm : z[(16 - i) & 15];
+        if (k < nkz) {
+          const T2 Z = z[i];
+          const long long o = zaddr(r, k);
+          fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
+          fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+        }
+      }
+    } else {
+    row_sync<TPRF>();
+    if (!(a.diag & 1)) wave_fft<NZP, RWW, PITCH, false, TPRF>(frow, twl, ft);
     {
       T2 z0[MKO] = {}, z1[MKO] = {};  // (zero-initialised: conditionally set arrays became loop-carried)
 #pragma unroll
@@ -534,6 +609,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
         }
       }
+    }
     }
     // the next row's first pair: in flight during this row's H_z transform and stores (and the
     // next row's start); issued here, after the Hx/Hy stores, it adds nothing to the register peak

@@ -71,11 +71,15 @@ def _assemble(parts, field):
 @pytest.mark.parametrize("world,pr,chunk,self_mode", [(2, 1, "0", "direct"), (3, 1, "0", "direct"),
                                                       (3, 1, "4", "direct"), (2, 1, "1", "direct"),
                                                       (3, 1, "4", "copy"), (2, 2, "0", "direct"),
-                                                      (4, 2, "0", "direct")])
+                                                      (4, 2, "0", "direct"), (4, 2, "4", "direct"),
+                                                      (4, 2, "5", "copy"), (6, 2, "3", "direct"),
+                                                      (6, 3, "4", "direct")])
 def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mode):
-    """chunk: y planes per exchange chunk of the slab pipeline (0 = whole slab; 4 with NY=33 over 3
-    ranks gives uneven ranks a different number of non-empty chunks); self_mode: own block in place
-    (direct) or copied inside the exchange (copy)."""
+    """chunk: y planes per exchange chunk of the slab and pencil pipelines (0 = whole slab; 4 with
+    NY=33 over 3 ranks gives uneven ranks a different number of non-empty chunks); self_mode: own
+    block in place (direct) or copied inside the exchange (copy).  pr > 1: pencil grids pr x
+    world/pr, the chunked software pipeline with the row-group (B) exchange on its own group
+    communicator."""
     monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
     monkeypatch.setenv("CHANNEL_A2A_SELF", self_mode)
     nsteps = 2
@@ -138,7 +142,7 @@ def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mo
             assert not any(f.endswith(".turn") for f in os.listdir(d))
 
 
-def _worker_big(rank, world, shm, outdir, grid, nsteps):
+def _worker_big(rank, world, shm, outdir, grid, nsteps, pr=1):
     import torch  # noqa: F401
 
     from channel_gpu_amd import require_native
@@ -146,7 +150,7 @@ def _worker_big(rank, world, shm, outdir, grid, nsteps):
 
     C = require_native()
     cfg = default_config(**grid, Re=2000.0, precision="fp64", ic="random", ic_amplitude=0.05, stats_every=0,
-                         log_every=0, symmetry_every=0)
+                         log_every=0, symmetry_every=0, decomposition="pencil" if pr > 1 else "slab", pr=pr)
     s = C.Solver(cfg, rank, world, 0, shm.encode())
     s.init_ic()  # deterministic and independent of P
     s.prepare()
@@ -159,17 +163,19 @@ def _worker_big(rank, world, shm, outdir, grid, nsteps):
     del s
 
 
-def test_eight_ranks_uneven_realistic_shape(native, monkeypatch):
-    """8 slab ranks at an uneven split like the headline's (NY = 385 over 8: 49/48 rows, 43 retained
-    kx over 8: 6/5 columns), y-chunked exchanges with a ragged last chunk: bitwise the single-rank
-    run (the arithmetic is identical; only the data movement differs)."""
+@pytest.mark.parametrize("pr", [1, 2])
+def test_eight_ranks_uneven_realistic_shape(native, monkeypatch, pr):
+    """8 ranks at an uneven split like the headline's, y-chunked exchanges with a ragged last chunk:
+    bitwise the single-rank run (the arithmetic is identical; only the data movement differs).
+    pr = 1: slab (NY = 385 over 8: 49/48 rows, 43 retained kx over 8: 6/5 columns); pr = 2: the
+    2 x 4 pencil (97/96 rows and 11/10 kx columns per process row, 22 kz and 64 x split in two)."""
     grid = dict(NX=64, NY=385, NZ=33)
     monkeypatch.setenv("CHANNEL_YCHUNK", "16")
     monkeypatch.setenv("CHANNEL_SHM_SLOT_MB", "8")
     world, nsteps = 8, 2
     shm = f"shm:chtest8_{uuid.uuid4().hex[:12]}"
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker_big, args=(world, shm, d, grid, nsteps), nprocs=world, join=True,
+        mp.start_processes(_worker_big, args=(world, shm, d, grid, nsteps, pr), nprocs=world, join=True,
                            start_method="spawn")
         parts = [dict(np.load(os.path.join(d, f"r{r}.npz"))) for r in range(world)]
     from channel_gpu_amd.utils.config import default_config
