@@ -12,6 +12,7 @@
 #   counters         rocprofv3 -L (available PMC counters) -> <TAG>_counter_names.txt
 #   configs          bench.py on every BASELINE config that fits one GPU
 #   rehearse2        2-rank torchrun bench on one GPU over the shared-memory loopback data plane
+#   rehearse8        8-rank bench.py --gpus 8 (slab, then pencil 2x4) over the loopback, headline grid
 #   ab               bench.py once per env setting in AB_ENVS ("A=1 B=2;A=2 B=2")
 #   probe            transform stage alone (tools/xform_probe.py $PROBE_ARGS) per env setting in PROBE_ENVS
 #   kprobe           rocprofv3 kernel stats of the transform stage on one stream (env: $KPROBE_ENV)
@@ -78,6 +79,14 @@ for step in "$@"; do
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --grid 256x129x256 \
         --re 3250 --steps 3 --warmup 1 > $log 2>&1 || fail rehearse2 $log
       tail -n 1 $log ;;
+    rehearse8)
+      # 8 ranks on the one GPU over the shared-memory loopback at the headline shape (bench.py
+      # self-launches torch.distributed.run): slab and the 2 x 4 pencil
+      for dec in slab pencil; do
+        CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus 8 --decomposition $dec --steps 2 --warmup 1 \
+          $BENCH_ARGS > gpurun_out/${tag}_rehearse8_$dec.log 2>&1 || fail "rehearse8 $dec" gpurun_out/${tag}_rehearse8_$dec.log
+        tail -n 1 gpurun_out/${tag}_rehearse8_$dec.log
+      done ;;
     ab)
       IFS=';' read -ra settings <<< "$AB_ENVS"
       i=0
