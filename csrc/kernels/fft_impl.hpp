@@ -120,6 +120,13 @@ inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
   return m >= NT / C ? kSegWin : kSegFull;
 }
 
+// V consecutive complex values moved by one global access (V = 2 for fp32: 16-byte loads and
+// stores, half the instructions of 8-byte ones; the stores of the x kernels were issue-bound)
+template <typename T2, int V>
+struct alignas(sizeof(T2) * V) CVec {
+  T2 c[V];
+};
+
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
 // LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
 // into registers right after the current tile is staged into LDS, so they are in flight during
@@ -127,15 +134,17 @@ inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
 // SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
 // compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
-template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
+  using CV = CVec<T2, V>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  constexpr int CW = C / V;  // accesses per tile row (V kz columns each; the host checks nkz % V == 0)
   // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
   constexpr int NKMAX = 2 * (NX / 3) + 1;
-  constexpr int EPT = (NKMAX * C + NT - 1) / NT;
+  constexpr int EPT = (NKMAX * CW + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
@@ -144,8 +153,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int ntiles = a.ny * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
-  const int nload = a.nkx * C;
-  T2 v[EPT];
+  const int nload = a.nkx * CW;
+  CV v[EPT];
   // tile t -> (f, y, kz0); at each iteration the blocks of one XCD take consecutive tiles
   auto fetch = [&](int t) {
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
@@ -158,16 +167,18 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int e = tid + q * NT;
       // unconditional load from a clamped valid address: rows i >= nkx are never staged,
       // columns kz >= nkz are transformed (independently) but never stored
-      const int i = min(e / C, a.nkx - 1);
-      const int kz = min(kz0 + e % C, a.nkz - 1);
+      const int i = min(e / CW, a.nkx - 1);
+      const int kz = min(kz0 + (e % CW) * V, a.nkz - V);
       if constexpr (SM == kSegOne) {
-        v[q] = base[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+        v[q] = *reinterpret_cast<const CV*>(
+            base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
       } else {
-        const SegPos sp = SM == kSegWin ? seg_find_win(src.kx_start, src.off, src.nsrc, (q * NT) / C, NT / C, i)
+        const SegPos sp = SM == kSegWin ? seg_find_win(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                         : seg_find(src.kx_start, src.off, src.nsrc, i);
         const T2* b = sp.idx == src.self_seg ? sbase : base;
         // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
-        v[q] = b[static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz)];
+        v[q] = *reinterpret_cast<const CV*>(
+            b + static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz));
       }
     }
   };
@@ -180,9 +191,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int i = e / C, c = e - i * C;
+      const int i = e / CW, c = (e - i * CW) * V;
       const int x = i <= a.Kx ? i : NX - (a.nkx - i);
-      if (e < nload) s[c * PITCH + fft_pidx(x)] = v[q];
+      if (e < nload)
+#pragma unroll
+        for (int u = 0; u < V; ++u) s[(c + u) * PITCH + fft_pidx(x)] = v[q].c[u];
     }
     for (int e = tid; e < (NX - a.nkx) * C; e += NT) {
       const int j = e / C, c = e - j * C;
@@ -204,29 +217,34 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
-    for (int e = tid; e < NX * C; e += NT) {
-      const int x = e / C, c = e - x * C;
+    for (int e = tid; e < NX * CW; e += NT) {
+      const int x = e / CW, c = (e - x * CW) * V;
       const int kz = kz0 + c;
       if (kz < a.nkz) {
+        CV w;
+#pragma unroll
+        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SEG) {
           const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
-          out[sp.off + (static_cast<long long>(y) * sp.count + (x - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(y) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
         } else {
-          out[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
-              s[c * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(out + static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) +
+                                 static_cast<unsigned>(kz)) = w;
         }
       }
     }
   }
 }
 
-template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull>
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
+  using CV = CVec<T2, V>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
-  constexpr int EPT = (NX * C + NT - 1) / NT;
+  constexpr int CW = C / V;
+  constexpr int EPT = (NX * CW + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
@@ -235,7 +253,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int ntiles = a.ny * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
-  T2 v[EPT];
+  CV v[EPT];
   auto fetch = [&](int t) {
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
     const int y = rest % a.ny, f = rest / a.ny;
@@ -243,14 +261,16 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int x = min(e / C, NX - 1);
-      const int kz = min(kz0 + e % C, a.nkz - 1);
+      const int x = min(e / CW, NX - 1);
+      const int kz = min(kz0 + (e % CW) * V, a.nkz - V);
       if constexpr (SEG) {
         const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
-        v[q] = in[static_cast<unsigned>(sp.off) +
-                  static_cast<unsigned>(y * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+        v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(sp.off) +
+                                            static_cast<unsigned>(y * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) +
+                                            static_cast<unsigned>(kz));
       } else {
-        v[q] = in[static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)];
+        v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) +
+                                            static_cast<unsigned>(kz));
       }
     }
   };
@@ -263,8 +283,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int x = e / C, c = e - x * C;
-      if (e < NX * C) s[c * PITCH + fft_pidx(x)] = v[q];
+      const int x = e / CW, c = (e - x * CW) * V;
+      if (e < NX * CW)
+#pragma unroll
+        for (int u = 0; u < V; ++u) s[(c + u) * PITCH + fft_pidx(x)] = v[q].c[u];
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
@@ -284,52 +306,90 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
     // this rank's own block goes straight into its spectral field (no self exchange)
     T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
-    for (int e0 = 0; e0 < a.nkx * C; e0 += NT) {
+    for (int e0 = 0; e0 < a.nkx * CW; e0 += NT) {
       const int e = e0 + tid;
-      const int i = e / C, c = e - i * C;
+      const int i = e / CW, c = (e - i * CW) * V;
       const int kz = kz0 + c;
-      if (e < a.nkx * C && kz < a.nkz) {
+      if (e < a.nkx * CW && kz < a.nkz) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+        CV w;
+#pragma unroll
+        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SM == kSegOne) {
-          outb[static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)] =
-              s[c * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
+                                 static_cast<unsigned>(kz)) = w;
         } else {
-          const SegPos sp = SM == kSegWin ? seg_find_win(dst.kx_start, dst.off, dst.ndst, e0 / C, NT / C, i)
+          const SegPos sp = SM == kSegWin ? seg_find_win(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
                                           : seg_find(dst.kx_start, dst.off, dst.ndst, i);
           T2* ob = sp.idx == dst.self_seg ? soutb : outb;
-          ob[sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz] = s[c * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz) = w;
         }
       }
     }
   }
 }
 
-template <int NN, typename T, int WIDE>
+// Persistent grid of a transform kernel: the resident capacity, or fewer blocks per CU when
+// CHANNEL_<NAME>_BPC sets it (A/B: room beside it for a concurrent kernel of the other stream)
+inline int persist_blocks(const void* kern, int threads, const char* env) {
+  int cap = resident_blocks(kern, threads);
+  if (const char* e = std::getenv(env)) {
+    const int bpc = std::atoi(e);
+    int dev = 0, cus = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (bpc > 0) cap = std::min(cap, bpc * cus);
+  }
+  return std::max(1, cap);
+}
+
+// 16-byte accesses (two fp32 complex per lane) need every element offset of a tile row even:
+// nkz even (rows start at multiples of nkz) and every block offset and field stride even
+inline bool xvec_ok(const XArgs& a, const long long* off, int n, long long self_stride, long long self_off) {
+  if (a.nkz % 2 || a.field_stride_spec % 2 || a.field_stride_phys % 2 || self_stride % 2 || self_off % 2) return false;
+  for (int i = 0; i < n; ++i)
+    if (off[i] % 2) return false;
+  for (int i = 0; i < a.npseg; ++i)
+    if (a.poff[i] % 2) return false;
+  static const bool off_env = [] {
+    const char* e = std::getenv("CHANNEL_XVEC");
+    return e && std::atoi(e) == 0;
+  }();
+  return !off_env;
+}
+
+template <int NN, typename T, int WIDE, int V = 1>
 static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
+  if constexpr (V == 1 && sizeof(T) == 4 && Cfg::C % 2 == 0) {
+    if (xvec_ok(a, src.off, src.nsrc, src.self_field_stride, 0)) return xb_launch_cfg<NN, T, WIDE, 2>(a, src, phys, tw, s);
+  }
   // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
   // its windows, computed up front, spilled ~640 SGPRs)
-  const int sm = seg_mode<Cfg::NT, Cfg::C>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
-  auto kern = a.npseg > 1     ? xfft_backward_kernel<NN, T, true, WIDE>
-              : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne>
-                              : xfft_backward_kernel<NN, T, false, WIDE, kSegFull>;
+  const int sm = seg_mode<Cfg::NT, Cfg::C / V>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
+  auto kern = a.npseg > 1     ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
+              : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
+                              : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
-  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
 }
 
-template <int NN, typename T, int WIDE>
+template <int NN, typename T, int WIDE, int V = 1>
 static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  const int sm = seg_mode<Cfg::NT, Cfg::C>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
-  auto kern = a.npseg > 1             ? xfft_forward_kernel<NN, T, true, WIDE>
-              : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne>
-              : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin>
-                              : xfft_forward_kernel<NN, T, false, WIDE, kSegFull>;
+  if constexpr (V == 1 && sizeof(T) == 4 && Cfg::C % 2 == 0) {
+    if (xvec_ok(a, dst.off, dst.ndst, dst.self_field_stride, 0)) return xf_launch_cfg<NN, T, WIDE, 2>(a, phys, dst, tw, s);
+  }
+  const int sm = seg_mode<Cfg::NT, Cfg::C / V>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
+  auto kern = a.npseg > 1             ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
+              : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
+              : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
+                              : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
-  dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), Cfg::NT)));
+  dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));
 }
@@ -966,7 +1026,7 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
   auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
                          : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
   const long long ngroups = (nrows + ZR - 1) / ZR;
-  const long long cap = zpers_enabled() ? resident_blocks(reinterpret_cast<const void*>(kern), ZR * TPR) : ngroups;
+  const long long cap = zpers_enabled() ? persist_blocks(reinterpret_cast<const void*>(kern), ZR * TPR, "CHANNEL_Z_BPC") : ngroups;
   dim3 grid(static_cast<unsigned>(std::min(ngroups, cap)));
   CH_CHECK(a.nkz <= NN / 3 + 1, "zphys: more retained kz than the 2/3 rule allows");
   CH_CHECK(TPR < 64 || nrows % ZR == 0, "zphys: rows per plane must be a multiple of the rows per block");
