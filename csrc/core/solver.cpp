@@ -167,10 +167,12 @@ void Solver::alloc() {
   physn_ = p.phys_elems();
   xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz_loc;
   zstride_ = p.pencil() ? p.zrow_elems() : 0;
-  HIP_CHECK(hipMalloc(&state_, 4 * spec_ * esz_));
+  // state_ = phi, R_phi, R_omega; the omega state is out_ field 4 (it IS the omega_y output of
+  // K-SPEC, which then stores one field less per substep; the x transform zeroes its mean line)
+  HIP_CHECK(hipMalloc(&state_, 3 * spec_ * esz_));
   HIP_CHECK(hipMalloc(&out_, 6 * spec_ * esz_));
   HIP_CHECK(hipMalloc(&phys_, std::max<size_t>(6 * physn_, 1) * esz_));
-  HIP_CHECK(hipMemset(state_, 0, 4 * spec_ * esz_));
+  HIP_CHECK(hipMemset(state_, 0, 3 * spec_ * esz_));
   HIP_CHECK(hipMemset(out_, 0, 6 * spec_ * esz_));
   if (comm_) {
     HIP_CHECK(hipMalloc(&xbuf_, 6 * xstride_ * esz_));
@@ -286,7 +288,9 @@ void Solver::free_all() {
 void* Solver::field_ptr(int f) const {
   char* st = static_cast<char*>(state_);
   char* ou = static_cast<char*>(out_);
-  if (f >= PHI && f <= ROMEGA) return st + static_cast<size_t>(f) * spec_ * esz_;
+  if (f == OMEGA) f = OUT4;
+  if (f == PHI) return st;
+  if (f == RPHI || f == ROMEGA) return st + static_cast<size_t>(f - RPHI + 1) * spec_ * esz_;
   if (f >= OUT0 && f <= OUT5) return ou + static_cast<size_t>(f - OUT0) * spec_ * esz_;
   CH_CHECK(false, "bad field index " << f);
 }
@@ -457,6 +461,7 @@ void Solver::kspec(int mode, int n, bool stats) {
     a.rk_b = RK3Coef::beta[n];
     a.rk_g = RK3Coef::gamma[n];
     a.rk_z = RK3Coef::zeta[n];
+    a.store_r = n < 2 ? 1 : 0;  // R of the last substep is never read (zeta[0] = 0)
   }
   a.dt = d_dt_;
   a.Q = cfg_.Q;
@@ -601,6 +606,8 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.nkz = p.nkz;
   xa.ny = p.ny_loc;
   xa.field_stride_phys = static_cast<long long>(physn_);
+  xa.zero_mean_field = 4;  // omega_y's spectral source is the omega state (mean line = U)
+  xa.kz_glob0 = p.kz0;
   ZArgs za;
   za.NX = p.NX;
   za.Nzp = p.Nzp;
@@ -764,7 +771,9 @@ void Solver::transforms(int n, bool /*stats*/) {
     HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_a2a_[f], 0));
     XSrc sf = src;
     sf.base = fld(xbuf_, xstride_, f);
-    xfft_backward(xa, sf, fld(phys_, physn_, f), tw_x_, fp64_, s_comp_);
+    XArgs xf1 = xa;
+    xf1.zero_mean_field = f == 4 ? 0 : -1;  // one field per call
+    xfft_backward(xf1, sf, fld(phys_, physn_, f), tw_x_, fp64_, s_comp_);
     if (pen) {  // ship field f's x-blocks to the row group while field f+1 is transformed
       HIP_CHECK(hipEventRecord(ev_b_[f], s_comp_));
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_b_[f], 0));
@@ -1601,7 +1610,8 @@ void Solver::take_snapshot() {
   const size_t fb = spec_ * esz_;
   if (!snap_) HIP_CHECK(hipMalloc(&snap_, 2 * fb + 2 * sizeof(double)));
   char* d = static_cast<char*>(snap_);
-  HIP_CHECK(hipMemcpyAsync(d, field_ptr(PHI), 2 * fb, hipMemcpyDeviceToDevice, s_comp_));  // PHI, OMEGA adjacent
+  HIP_CHECK(hipMemcpyAsync(d, field_ptr(PHI), fb, hipMemcpyDeviceToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(d + fb, field_ptr(OMEGA), fb, hipMemcpyDeviceToDevice, s_comp_));
   HIP_CHECK(hipMemcpyAsync(d + 2 * fb, d_dt_, 2 * sizeof(double), hipMemcpyDeviceToDevice, s_comp_));
   snap_step_ = nstep_;
 }
@@ -1611,7 +1621,8 @@ void Solver::rollback() {
   synchronize();
   const size_t fb = spec_ * esz_;
   char* d = static_cast<char*>(snap_);
-  HIP_CHECK(hipMemcpyAsync(field_ptr(PHI), d, 2 * fb, hipMemcpyDeviceToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(field_ptr(PHI), d, fb, hipMemcpyDeviceToDevice, s_comp_));
+  HIP_CHECK(hipMemcpyAsync(field_ptr(OMEGA), d + fb, fb, hipMemcpyDeviceToDevice, s_comp_));
   HIP_CHECK(hipMemcpyAsync(d_dt_, d + 2 * fb, 2 * sizeof(double), hipMemcpyDeviceToDevice, s_comp_));
   HIP_CHECK(hipMemsetAsync(field_ptr(RPHI), 0, 2 * fb, s_comp_));  // zeta_0 = 0: R is not needed at substep 0
   HIP_CHECK(hipMemsetAsync(d_max_, 0, 4 * sizeof(float), s_comp_));

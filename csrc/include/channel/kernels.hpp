@@ -73,6 +73,9 @@ struct SpecArgs {
   void* Rphi = nullptr;
   void* Romega = nullptr;
   void* out[6] = {};      // u, v, w, omega_x, omega_y, omega_z ; out[0..2] double as H_x,H_y,H_z input
+                          // (out[4] == omega: the state IS the omega_y output, nothing is stored
+                          // there; the x transform zeroes its mean line, see XArgs::zero_mean_field)
+  int store_r = 1;        // 0: skip the R_phi/R_omega stores (last substep: the next one has zeta = 0)
   // diagnostics
   double* stats = nullptr;   // [4][N] plane sums (uu, vv, ww, uv) when non-null
   double* mean_diag = nullptr;  // [3N + 8]: U, Nx, dU/dy(walls), flux, pressure gradient ...
@@ -127,6 +130,11 @@ struct XArgs {
   int x_start[9] = {0};
   long long poff[8] = {0};
   int diag = 0;                      // bit 0: skip the transforms (timing diagnosis, CHANNEL_FFT_DIAG)
+  // backward only: field zero_mean_field's (kx = 0, kz = 0) element is read as 0 (omega_y: the
+  // spectral source is the omega state, whose mean line holds U(y)); kz_glob0 = global kz of local
+  // kz 0 (pencil rows)
+  int zero_mean_field = -1;
+  int kz_glob0 = 0;
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);

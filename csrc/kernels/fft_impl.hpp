@@ -188,6 +188,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     const int kz0 = (t % nkzc) * C, rest = t / nkzc;
     const int y = rest % a.ny, f = rest / a.ny;
     lds_barrier();  // previous tile's stores have finished reading s
+    // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
+    // state, whose mean line holds U(y)); it is e = 0: thread 0, q = 0, u = 0
+    const bool zmean = f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -195,7 +198,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int x = i <= a.Kx ? i : NX - (a.nkx - i);
       if (e < nload)
 #pragma unroll
-        for (int u = 0; u < V; ++u) s[(c + u) * PITCH + fft_pidx(x)] = v[q].c[u];
+        for (int u = 0; u < V; ++u)
+          s[(c + u) * PITCH + fft_pidx(x)] = (q == 0 && u == 0 && zmean && e == 0) ? T2{0, 0} : v[q].c[u];
     }
     for (int e = tid; e < (NX - a.nkx) * C; e += NT) {
       const int j = e / C, c = e - j * C;

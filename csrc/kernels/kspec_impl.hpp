@@ -464,8 +464,10 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         }
       }
       KSPEC_STAMP(1)
-      st.store(Rphi, RPn);
-      st.store(Romega, RWn);
+      if (a.store_r) {  // (the last substep's R is never read: the next substep has zeta = 0)
+        st.store(Rphi, RPn);
+        st.store(Romega, RWn);
+      }
       KSPEC_STAMP(2)
 
       // ---------------- implicit viscous solves (phi, omega share one factorisation) -------
@@ -706,8 +708,10 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       __syncthreads();  // sred is a staging tile again
     }
     KSPEC_STAMP(8)
-    st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);                   // v
-    st.store(static_cast<T2*>(a.out[4]), vo[2], vo[3], 1.0 - mf);         // omega_y (0 on the mean line)
+    st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);  // v
+    // omega_y: when out[4] is the omega state itself (the solver's layout) it is already stored;
+    // the x transform reads its mean line (U) as 0
+    if (a.out[4] != a.omega) st.store(static_cast<T2*>(a.out[4]), vo[2], vo[3], 1.0 - mf);
     {
       double x[2][R];
 #pragma unroll
