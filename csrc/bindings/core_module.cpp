@@ -124,6 +124,8 @@ PYBIND11_MODULE(_core, m) {
   m.def("new_unique_id", &new_uid);
   m.def("hdf5_available", &hdf5_available);
   m.def("set_debug_sync", &set_debug_sync);
+  m.def("set_lds_poison", &set_lds_poison);
+  m.def("lds_poison_enabled", &lds_poison_enabled);
   m.def("install_crash_handler", &install_crash_handler, "native backtrace on fatal signals (stderr)");
   m.def("h5_create_field", &h5_create_field, py::arg("path"), py::arg("NX"), py::arg("NY"), py::arg("NZ"),
         py::arg("fp64") = false, py::arg("Kx") = -1);

@@ -88,6 +88,12 @@ void install_crash_handler() {
 
 bool debug_sync_enabled() { return g_debug_sync; }
 void set_debug_sync(bool on) { g_debug_sync = on; }
+bool g_lds_poison = [] {
+  const char* e = std::getenv("CHANNEL_LDS_POISON");
+  return e && std::atoi(e) != 0;
+}();
+bool lds_poison_enabled() { return g_lds_poison; }
+void set_lds_poison(bool on) { g_lds_poison = on; }
 
 int resident_blocks(const void* kernel, int threads, size_t dyn_lds) {
   static std::mutex mu;
@@ -478,6 +484,7 @@ void Solver::kspec(int mode, int n, bool stats) {
   a.mean_diag = p.owns_mean() ? d_mean_ : nullptr;
   a.health = cfg_.health_check ? d_health_ : nullptr;
   a.prof = kprof_on_ ? d_kprof_ : nullptr;
+  a.lds_poison = lds_poison_enabled() ? 1 : 0;
   if (stats) HIP_CHECK(hipMemsetAsync(d_stats_, 0, 4 * p.NY * sizeof(double), s_comp_));
   ev(0, false);
   // (measured r2s: splitting this fused pass into an advance kernel and a prepare kernel frees no
@@ -608,7 +615,9 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.field_stride_phys = static_cast<long long>(physn_);
   xa.zero_mean_field = 4;  // omega_y's spectral source is the omega state (mean line = U)
   xa.kz_glob0 = p.kz0;
+  xa.lds_poison = lds_poison_enabled() ? 1 : 0;
   ZArgs za;
+  za.lds_poison = xa.lds_poison;
   za.NX = p.NX;
   za.Nzp = p.Nzp;
   za.nkz = p.nkz;

@@ -29,6 +29,11 @@ struct Error : std::runtime_error {
 // that caused them (the reference's kernelCheck ran cudaGetLastError without a sync, check.cu:7).
 bool debug_sync_enabled();
 void set_debug_sync(bool on);
+// LDS poison-fill debug mode (CHANNEL_LDS_POISON=1 or set_lds_poison): the hot kernels fill their
+// shared memory with NaN bit patterns before any use, so a read of an LDS slot that the kernel
+// never wrote turns the result into NaN instead of silently reusing stale data
+bool lds_poison_enabled();
+void set_lds_poison(bool on);
 // SIGSEGV/SIGBUS/SIGABRT handler that writes the native backtrace (execinfo) to stderr before the
 // process dies (failure diagnosis on boxes without a debugger); CHANNEL_CRASH_TRACE=1 installs it
 // at library load

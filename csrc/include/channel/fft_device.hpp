@@ -529,6 +529,14 @@ __device__ __forceinline__ void wave_fft_half(T2* __restrict__ buf, const T2* __
 }
 
 
+// LDS poison fill (debug): every 32-bit word of [p, p + bytes) becomes 0xFFFFFFFF, a
+// NaN as float and as double, so data read from a slot the kernel never wrote propagates as NaN.
+// Block-cooperative; the caller synchronises before the first real use.
+__device__ __forceinline__ void lds_poison_fill(void* p, int bytes) {
+  unsigned* w = static_cast<unsigned*>(p);
+  for (int i = threadIdx.x; i < bytes / 4; i += blockDim.x) w[i] = 0xFFFFFFFFu;
+}
+
 // XCD-aware block remap (cdna_hip_programming.md T1): blocks b and b+8 share an XCD under the
 // observed round-robin dispatch, so logical tiles that are adjacent in memory are given to blocks
 // on the same XCD (their partial cache lines then merge in one L2).  Bijective for any n.

@@ -76,6 +76,7 @@ struct SpecArgs {
                           // (out[4] == omega: the state IS the omega_y output, nothing is stored
                           // there; the x transform zeroes its mean line, see XArgs::zero_mean_field)
   int store_r = 1;        // 0: skip the R_phi/R_omega stores (last substep: the next one has zeta = 0)
+  int lds_poison = 0;     // debug: fill the LDS with NaN before use (CHANNEL_LDS_POISON)
   // diagnostics
   double* stats = nullptr;   // [4][N] plane sums (uu, vv, ww, uv) when non-null
   double* mean_diag = nullptr;  // [3N + 8]: U, Nx, dU/dy(walls), flux, pressure gradient ...
@@ -135,6 +136,7 @@ struct XArgs {
   // kz 0 (pencil rows)
   int zero_mean_field = -1;
   int kz_glob0 = 0;
+  int lds_poison = 0;                // debug: fill the LDS with NaN before use
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
@@ -154,6 +156,7 @@ struct ZArgs {
   const double* inv_dy = nullptr;    // [NY] 1/local spacing for the CFL estimate
   double cx = 0, cz = 0;             // kx_max, kz_max for the CFL estimate
   float* maxima = nullptr;           // [4]: |u|max, |v|max, |w|max, cfl sum max (atomicMax)
+  int lds_poison = 0;                // debug: fill the LDS with NaN before use
 };
 // physical-space stage: 6 fields (u,v,w,wx,wy,wz) [y][x][kz] -> z C2R -> H = u x omega -> z R2C
 // -> truncated H_x,H_y,H_z written in place over fields 0..2.

@@ -148,6 +148,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
+  if (a.lds_poison) {
+    lds_poison_fill(s, sizeof(s));
+    lds_poison_fill(tws, sizeof(tws));
+    __syncthreads();
+  }
   for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const int ntiles = a.ny * nkzc * a.nfields;
@@ -252,6 +257,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
+  if (a.lds_poison) {
+    lds_poison_fill(s, sizeof(s));
+    lds_poison_fill(tws, sizeof(tws));
+    __syncthreads();
+  }
   for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
   const int nkzc = (a.nkz + C - 1) / C;
   const int ntiles = a.ny * nkzc * a.nfields;
@@ -449,6 +459,12 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   // lane: wave lane (reductions); t: thread within the row; w: row within the block
   const int tid = threadIdx.x, lane = tid & 63;
   int t = tid % TPR, w = tid / TPR;
+  if (a.lds_poison) {
+    lds_poison_fill(s, sizeof(s));
+    lds_poison_fill(tws, sizeof(tws));
+    lds_poison_fill(red, sizeof(red));
+    __syncthreads();
+  }
   for (int i = tid; i < TSA; i += ZWT * TPR) tws[i] = tw[i];
   __syncthreads();
   T2* row = s + w * PITCH;

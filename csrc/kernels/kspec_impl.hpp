@@ -234,6 +234,12 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const int lane = __lane_id();
   const int w = threadIdx.x / 64;
   const int N = a.N;
+  if (a.lds_poison) {
+    lds_poison_fill(tab_lds, sizeof(tab_lds));
+    lds_poison_fill(tile_mem, sizeof(tile_mem));
+    lds_poison_fill(xs_mem, sizeof(xs_mem));
+    __syncthreads();
+  }
   if constexpr (TLDS) {
     // coefficient tables (13 per-row tables + the D1 factorisation, contiguous from d1_lo) staged
     // once per block: every solve step reads them, and from L2 each read is a dependent load

@@ -382,3 +382,33 @@ def test_fp32_tracks_fp64_on_resolved_modes(native):
     print(f"U: rel {dU:.3e}")
     assert worst["phi"] < 2e-5 and worst["omega"] < 2e-5, worst
     assert dU < 1e-6
+
+
+@pytest.mark.parametrize("precision,NX,NY,NZ", [("fp32", 32, 33, 17), ("fp32", 64, 385, 33), ("fp64", 32, 129, 17),
+                                                ("fp32", 48, 97, 41)])
+def test_lds_poison_mode_is_bitwise(native, precision, NX, NY, NZ):
+    """LDS poison-fill debug mode: K-SPEC, the x transforms and the z stage fill their
+    shared memory with NaN bit patterns before use.  A kernel that read a slot it never wrote would
+    turn NaN (or at least differ); the run must equal the normal one bitwise."""
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=2000.0, precision=precision, ic="random", ic_amplitude=0.05,
+              stats_every=1, log_every=0, symmetry_every=0, dt_fixed=2e-4)
+    res = []
+    try:
+        for poison in (False, True):
+            native.set_lds_poison(poison)
+            assert native.lds_poison_enabled() == poison
+            s = make_solver(native, **kw)
+            s.init_ic()
+            s.prepare()
+            for _ in range(3):
+                s.step(True)
+            assert s.health() == 0
+            res.append((s.get_state(), np.asarray(s.stats())))
+            del s
+    finally:
+        native.set_lds_poison(False)
+    (a, sa), (b, sb) = res
+    for f in range(3):
+        assert np.all(np.isfinite(b[f]))
+        assert np.array_equal(a[f], b[f]), f"field {f}"
+    assert np.allclose(sa, sb, rtol=1e-12, atol=0)  # (plane sums: atomic order may differ)
