@@ -48,7 +48,8 @@ HEADLINE_METRIC = "wall-sec/RK3-step + grid-pts/sec at Re_tau=950, 1024x385x1024
 STATS_EVERY = 10
 # xGMI model: one link per peer pair, ~153 GB/s per link (point-to-point, no switch)
 XGMI_LINK_GBPS = 153.0
-PHASES = ["kspec", "x_backward", "z_physical", "x_forward", "a2a", "reduce", "io", "other"]
+# slot 7: milliseconds in which a K-SPEC interval and an exchange interval ran at once (P > 1)
+PHASES = ["kspec", "x_backward", "z_physical", "x_forward", "a2a", "reduce", "io", "kspec_a2a_overlap"]
 
 
 def _free_port() -> int:

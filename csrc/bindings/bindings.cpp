@@ -168,6 +168,8 @@ std::pair<torch::Tensor, torch::Tensor> zphys_op(torch::Tensor fields, int Nzp, 
 
 torch::Tensor field_tensor(Solver& s, int f) {
   const Plan& p = s.plan();
+  // a [y][kx][kz] view only exists for the plain layout (kx sub-blocks: use get_state)
+  CH_CHECK(s.kblocks() == 1, "field(): the spectral fields are stored as " << s.kblocks() << " kx sub-blocks");
   auto opts = torch::TensorOptions()
                   .dtype(s.fp64() ? torch::kComplexDouble : torch::kComplexFloat)
                   .device(torch::kCUDA, c10::hip::current_device());

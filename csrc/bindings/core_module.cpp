@@ -188,6 +188,7 @@ PYBIND11_MODULE(_core, m) {
       .def("synchronize", &Solver::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("log", &Solver::log, py::call_guard<py::gil_scoped_release>())
       .def("stats", [](Solver& s) { return vec(s.stats()); })
+      .def("kblocks", &Solver::kblocks)
       .def("mean_profile", [](Solver& s) { return vec(s.mean_profile()); })
       .def("health", &Solver::health)
       .def("time", &Solver::time)

@@ -171,6 +171,25 @@ void Solver::alloc() {
   const Plan& p = plan_;
   spec_ = p.spec_elems();
   physn_ = p.phys_elems();
+  // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
+  // every rank (a function of Pc and the environment), at most 8 exchange segments in total
+  nkb_ = 1;
+  if (comm_ && !p.pencil()) {
+    int want = p.Pc <= 2 ? 4 : (p.Pc <= 4 ? 2 : 1);
+    if (const char* e = std::getenv("CHANNEL_KBLOCKS")) want = std::atoi(e);
+    int minc = p.nkx;
+    for (int c = 0; c < p.Pc; ++c) minc = std::min(minc, p.kx_split.count[c]);
+    nkb_ = std::max(1, std::min({want, 8 / p.Pc, minc}));
+  }
+  {
+    const Split kb = Split::balanced(p.nkx_loc, nkb_);
+    kb_start_ = kb.start;
+    kb_cnt_ = kb.count;
+    kb_off_.assign(nkb_, 0);
+    for (int b = 1; b < nkb_; ++b) kb_off_[b] = kb_off_[b - 1] + static_cast<size_t>(p.NY) * kb_cnt_[b - 1] * p.nkz_loc;
+    ev_kb_.resize(nkb_);
+    for (auto& e : ev_kb_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz_loc;
   zstride_ = p.pencil() ? p.zrow_elems() : 0;
   // state_ = phi, R_phi, R_omega; the omega state is out_ field 4 (it IS the omega_y output of
@@ -267,8 +286,9 @@ void Solver::free_all() {
   for (auto st : s_extra_) (void)hipStreamDestroy(st);
   ev_join_.clear();
   s_extra_.clear();
-  for (auto* v : {&ev_cb_, &ev_cc_})
+  for (auto* v : {&ev_cb_, &ev_cc_, &ev_kb_})
     for (auto e : *v) (void)hipEventDestroy(e);
+  ev_kb_.clear();
   for (auto& v : ev_pen_) {
     for (auto e : v) (void)hipEventDestroy(e);
     v.clear();
@@ -301,6 +321,16 @@ void* Solver::field_ptr(int f) const {
   CH_CHECK(false, "bad field index " << f);
 }
 
+int Solver::kb_gstart(int c, int b) const {
+  return plan_.kx_split.start[c] + Split::balanced(plan_.kx_split.count[c], nkb_).start[b];
+}
+int Solver::kb_gcount(int c, int b) const { return Split::balanced(plan_.kx_split.count[c], nkb_).count[b]; }
+size_t Solver::kb_index(int y, int ikx, int kz) const {
+  int b = nkb_ - 1;
+  while (b > 0 && ikx < kb_start_[b]) --b;
+  return kb_off_[b] + (static_cast<size_t>(y) * kb_cnt_[b] + (ikx - kb_start_[b])) * plan_.nkz_loc + kz;
+}
+
 // ---- state ------------------------------------------------------------------------------------
 void Solver::set_state(const std::complex<double>* phi, const std::complex<double>* omega, const double* U) {
   const Plan& p = plan_;
@@ -308,6 +338,20 @@ void Solver::set_state(const std::complex<double>* phi, const std::complex<doubl
   std::vector<std::complex<double>> om(omega, omega + spec_);
   if (p.owns_mean()) {
     for (int j = 0; j < p.NY; ++j) om[static_cast<size_t>(j) * lines] = std::complex<double>(U ? U[j] : 0.0, 0.0);
+  }
+  std::vector<std::complex<double>> phb;
+  if (nkb_ > 1) {  // [y][kx_local][kz] -> kx sub-blocks
+    phb.resize(spec_);
+    std::vector<std::complex<double>> omb(spec_);
+    for (int y = 0; y < p.NY; ++y)
+      for (int i = 0; i < p.nkx_loc; ++i)
+        for (int k = 0; k < p.nkz_loc; ++k) {
+          const size_t src = (static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k, dst = kb_index(y, i, k);
+          phb[dst] = phi[src];
+          omb[dst] = om[src];
+        }
+    om.swap(omb);
+    phi = phb.data();
   }
   HIP_CHECK(hipStreamSynchronize(s_comp_));
   if (fp64_) {
@@ -343,6 +387,14 @@ void Solver::get_state(std::complex<double>* phi, std::complex<double>* omega, d
   };
   fetch(PHI, phi);
   fetch(OMEGA, omega);
+  if (nkb_ > 1) {  // kx sub-blocks -> [y][kx_local][kz]
+    for (auto* q : {phi, omega}) {
+      std::vector<std::complex<double>> t(q, q + spec_);
+      for (int y = 0; y < p.NY; ++y)
+        for (int i = 0; i < p.nkx_loc; ++i)
+          for (int k = 0; k < p.nkz_loc; ++k) q[(static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k] = t[kb_index(y, i, k)];
+    }
+  }
   const int lines = p.lines_loc();
   for (int j = 0; j < p.NY; ++j) {
     if (p.owns_mean()) {
@@ -489,7 +541,27 @@ void Solver::kspec(int mode, int n, bool stats) {
   ev(0, false);
   // (measured r2s: splitting this fused pass into an advance kernel and a prepare kernel frees no
   // occupancy at R = 7 -- 481 and 348 registers -- and costs 10.2 vs 7.2 ms per substep)
-  kspec_launch(ytab_, a, fp64_, s_comp_);
+  if (nkb_ == 1) {
+    kspec_launch(ytab_, a, fp64_, s_comp_);
+  } else {
+    // kx sub-block b: the lines of local kx [kb_start_[b], +kb_cnt_[b]), a [y][lines_b] region of
+    // every field; ev_kb_[b] lets the comm stream send block b while block b+1 is solved
+    for (int b = 0; b < nkb_; ++b) {
+      SpecArgs ab = a;
+      const size_t off = kb_off_[b] * esz_;
+      auto sh = [&](void* q) { return static_cast<void*>(static_cast<char*>(q) + off); };
+      ab.lines = kb_cnt_[b] * p.nkz_loc;
+      ab.kx0 = p.kx0 + kb_start_[b];
+      ab.phi = sh(a.phi);
+      ab.omega = sh(a.omega);
+      ab.Rphi = sh(a.Rphi);
+      ab.Romega = sh(a.Romega);
+      for (int i = 0; i < 6; ++i) ab.out[i] = sh(a.out[i]);
+      ab.mean_diag = b == 0 ? a.mean_diag : nullptr;  // (kx = 0 is local kx 0: block 0)
+      kspec_launch(ytab_, ab, fp64_, s_comp_);
+      HIP_CHECK(hipEventRecord(ev_kb_[b], s_comp_));
+    }
+  }
   ev(0, true);
   if (stats && comm_) {
     HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
@@ -562,11 +634,24 @@ hipEvent_t Solver::timing_event() {
 void Solver::flush_phase_events() {
   if (!tpairs_.empty()) {
     synchronize();
+    // intervals on a common clock (relative to the first event of the step): durations per phase,
+    // and in slot 7 the time K-SPEC (phase 0, compute stream) and the exchanges (phase 4, comm
+    // stream) actually ran at once (the K-SPEC / exchange overlap of the kx sub-blocks)
+    std::vector<std::pair<float, float>> ks, ex;
     for (const auto& t : tpairs_) {
-      float ms = 0;
+      float ms = 0, a0 = 0, b0 = 0;
       HIP_CHECK(hipEventElapsedTime(&ms, t.a, t.b));
       ph_ms_[t.phase] += ms;
+      if (t.phase == 0 || t.phase == 4) {
+        HIP_CHECK(hipEventElapsedTime(&a0, tpairs_[0].a, t.a));
+        HIP_CHECK(hipEventElapsedTime(&b0, tpairs_[0].a, t.b));
+        (t.phase == 0 ? ks : ex).push_back({a0, b0});
+      }
     }
+    double ov = 0.0;
+    for (const auto& k : ks)
+      for (const auto& e : ex) ov += std::max(0.0f, std::min(k.second, e.second) - std::max(k.first, e.first));
+    ph_ms_[7] += ov;
   }
   tpairs_.clear();
   tev_used_ = 0;
@@ -846,42 +931,51 @@ void Solver::transforms(int n, bool /*stats*/) {
 // of my chunk go back into the owners' spectral rows.  Both sides are contiguous in memory, so
 // there is no pack/unpack pass (the reference ran 5 cublasCgeam passes around each host-staged
 // MPI_Alltoall, channel_cuda_mpi.c:64-128).
-void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) {
+void Solver::a2a_slab_chunk(int k, int ch, bool to_phys, int nf) { a2a_slab_rows(k * ch, ch, to_phys, nf, 0, nkb_); }
+
+// Rows [r0, r0 + nr) of every rank's y range, kx sub-blocks [blo, bhi): one op per (field, block),
+// each with one contiguous piece per peer (block b of the spectral field is [y][lines_b]; the
+// receive segment (c, b) of xbuf is [y_loc][kx in block b of rank c][kz] in global kx order).
+void Solver::a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bhi) {
   const Plan& p = plan_;
-  const int P = p.Pc, lines = p.lines_loc();  // column group (slab: the world)
-  const size_t nr_me = static_cast<size_t>(std::max(0, std::min(ch, p.ny_loc - k * ch)));
-  std::vector<A2ABlock> ops(nf);
-  for (int f = 0; f < nf; ++f) {
-    A2ABlock& o = ops[f];
-    o.scount.assign(P, 0);
-    o.soff.assign(P, 0);
-    o.rcount.assign(P, 0);
-    o.roff.assign(P, 0);
-    char* spec = static_cast<char*>(field_ptr(OUT0 + f));
-    char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-    for (int c = 0; c < P; ++c) {
-      if (self_direct_ && c == p.pcol) continue;  // read/written in place by the x transforms
-      const size_t nr_c = static_cast<size_t>(std::max(0, std::min(ch, p.y_split.count[c] - k * ch)));
-      const size_t yo = (static_cast<size_t>(p.y_split.start[c]) + static_cast<size_t>(k) * ch) * lines * esz_;
-      const size_t yc = nr_c * lines * esz_;
-      const size_t xo = (static_cast<size_t>(p.ny_loc) * p.kx_split.start[c] +
-                         static_cast<size_t>(k) * ch * p.kx_split.count[c]) * p.nkz_loc * esz_;
-      const size_t xc = nr_me * p.kx_split.count[c] * p.nkz_loc * esz_;
-      if (to_phys) {
-        o.soff[c] = yc ? yo : 0;
-        o.scount[c] = yc;
-        o.roff[c] = xc ? xo : 0;
-        o.rcount[c] = xc;
-      } else {
-        o.soff[c] = xc ? xo : 0;
-        o.scount[c] = xc;
-        o.roff[c] = yc ? yo : 0;
-        o.rcount[c] = yc;
+  const int P = p.Pc;  // column group (slab: the world)
+  const size_t nr_me = static_cast<size_t>(std::max(0, std::min(nr, p.ny_loc - r0)));
+  std::vector<A2ABlock> ops;
+  ops.reserve(static_cast<size_t>(nf) * (bhi - blo));
+  for (int f = 0; f < nf; ++f)
+    for (int b = blo; b < bhi; ++b) {
+      ops.emplace_back();
+      A2ABlock& o = ops.back();
+      o.scount.assign(P, 0);
+      o.soff.assign(P, 0);
+      o.rcount.assign(P, 0);
+      o.roff.assign(P, 0);
+      char* spec = static_cast<char*>(field_ptr(OUT0 + f));
+      char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
+      const size_t lines_b = static_cast<size_t>(kb_cnt_[b]) * p.nkz_loc;
+      for (int c = 0; c < P; ++c) {
+        if (self_direct_ && c == p.pcol) continue;  // read/written in place by the x transforms
+        const size_t nr_c = static_cast<size_t>(std::max(0, std::min(nr, p.y_split.count[c] - r0)));
+        const size_t yo = (kb_off_[b] + (static_cast<size_t>(p.y_split.start[c]) + r0) * lines_b) * esz_;
+        const size_t yc = nr_c * lines_b * esz_;
+        const size_t gs = static_cast<size_t>(kb_gstart(c, b)), gc = static_cast<size_t>(kb_gcount(c, b));
+        const size_t xo = (static_cast<size_t>(p.ny_loc) * gs + static_cast<size_t>(r0) * gc) * p.nkz_loc * esz_;
+        const size_t xc = nr_me * gc * p.nkz_loc * esz_;
+        if (to_phys) {
+          o.soff[c] = yc ? yo : 0;
+          o.scount[c] = yc;
+          o.roff[c] = xc ? xo : 0;
+          o.rcount[c] = xc;
+        } else {
+          o.soff[c] = xc ? xo : 0;
+          o.scount[c] = xc;
+          o.roff[c] = yc ? yo : 0;
+          o.rcount[c] = yc;
+        }
       }
+      o.send = to_phys ? static_cast<const void*>(spec) : static_cast<const void*>(xb);
+      o.recv = to_phys ? static_cast<void*>(xb) : static_cast<void*>(spec);
     }
-    o.send = to_phys ? static_cast<const void*>(spec) : static_cast<const void*>(xb);
-    o.recv = to_phys ? static_cast<void*>(xb) : static_cast<void*>(spec);
-  }
   col_comm()->alltoallv_batch(ops, s_comm_);
 }
 
@@ -908,16 +1002,21 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   XArgs xa = xa0;
   xa.nkz = p.nkz_loc;
   xa.field_stride_spec = static_cast<long long>(xstride_);
+  // exchange segments: block b of rank c is segment c * nkb_ + b (global kx order)
+  const int NB = nkb_, NS = P * NB;
+  CH_CHECK(NS <= 8, "at most 8 exchange segments");
   XSrc src;
   src.base = xbuf_;
-  src.nsrc = P;
+  src.nsrc = NS;
   XDst dst;
   dst.base = xbuf_;
-  dst.ndst = P;
-  for (int c = 0; c < P; ++c) src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
-  src.kx_start[P] = dst.kx_start[P] = p.nkx;
-  if (self_direct_) {  // own kx block: straight from / into the spectral fields
-    src.self_seg = dst.self_seg = p.rank;
+  dst.ndst = NS;
+  for (int c = 0; c < P; ++c)
+    for (int b = 0; b < NB; ++b) src.kx_start[c * NB + b] = dst.kx_start[c * NB + b] = kb_gstart(c, b);
+  src.kx_start[NS] = dst.kx_start[NS] = p.nkx;
+  if (self_direct_) {  // own kx blocks: straight from / into the spectral fields
+    src.self_seg = dst.self_seg = p.rank * NB;
+    src.nself = dst.nself = NB;
     src.self_base = out_;
     dst.self_base = out_;
     src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
@@ -925,11 +1024,28 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   }
 
   roctxRangePushA("xzx_slab_chunked");
-  HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
-  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  // K-SPEC / exchange overlap: blocks 0 .. NB-2 of the previous substep's K-SPEC go out whole as
+  // soon as each is solved (while the next block runs on the compute stream); the last block is
+  // sent chunk by chunk ahead of the transforms.  Substep 0 of a step starts without the overlap:
+  // its K-SPEC belongs to the previous step (another graph launch), whose events this step's
+  // capture cannot wait on.
+  const bool overlap = NB > 1 && n > 0;
+  const int bchunk = overlap ? NB - 1 : 0;  // blocks still to send per chunk: [bchunk, NB)
+  if (overlap) {
+    for (int b = 0; b + 1 < NB; ++b) {
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
+      ev(4, false, s_comm_);
+      a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+      ev(4, true, s_comm_);
+    }
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
+  } else {
+    HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  }
   auto backward = [&](int k) {
     ev(4, false, s_comm_);
-    a2a_slab_chunk(k, ch, true, 6);
+    a2a_slab_rows(k * ch, ch, true, 6, bchunk, NB);
     ev(4, true, s_comm_);
     HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
   };
@@ -940,10 +1056,13 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     const int y0 = k * ch, ny = std::max(0, std::min(ch, p.ny_loc - y0));
     if (ny > 0) {
       for (int c = 0; c < P; ++c)
-        src.off[c] = dst.off[c] = (static_cast<long long>(p.ny_loc) * p.kx_split.start[c] +
-                                   static_cast<long long>(y0) * p.kx_split.count[c]) * p.nkz_loc;
-      if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields
-        src.off[p.rank] = dst.off[p.rank] = (static_cast<long long>(p.y0) + y0) * p.lines_loc();
+        for (int b = 0; b < NB; ++b)
+          src.off[c * NB + b] = dst.off[c * NB + b] =
+              (static_cast<long long>(p.ny_loc) * kb_gstart(c, b) + static_cast<long long>(y0) * kb_gcount(c, b)) * p.nkz_loc;
+      if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields (block b)
+        for (int b = 0; b < NB; ++b)
+          src.off[p.rank * NB + b] = dst.off[p.rank * NB + b] =
+              static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * p.nkz_loc;
       XArgs xc = xa;
       xc.ny = ny;
       xc.nfields = 6;
@@ -1423,8 +1542,11 @@ void Solver::symmetrize() {
         o.roff[g] = static_cast<size_t>(p.NY) * p.kx_split.start[c] * esz_;
       }
     }
-    if (has_kz0)
-      kz0_pack(field_ptr(f == 0 ? PHI : OMEGA), col_loc + f * loc * esz_, p.NY, p.nkx_loc, p.nkz_loc, fp64_, s_comp_);
+    if (has_kz0)  // per kx sub-block: col_loc = [b][y][kx in b], i.e. global kx order again
+      for (int b = 0; b < nkb_; ++b)
+        kz0_pack(static_cast<char*>(field_ptr(f == 0 ? PHI : OMEGA)) + kb_off_[b] * esz_,
+                 col_loc + (f * loc + static_cast<size_t>(p.NY) * kb_start_[b]) * esz_, p.NY, kb_cnt_[b], p.nkz_loc,
+                 fp64_, s_comp_);
   }
   HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
   HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_stats_, 0));
@@ -1434,14 +1556,19 @@ void Solver::symmetrize() {
   if (has_kz0) {
     Kz0SymArgs a;
     a.N = p.NY;
-    a.nkx_loc = p.nkx_loc;
     a.nkz_loc = p.nkz_loc;
-    a.kx0 = p.kx0;
     a.nkx = p.nkx;
-    a.nblk = p.Pc;
-    for (int c = 0; c <= p.Pc; ++c) a.kx_start[c] = c < p.Pc ? p.kx_split.start[c] : p.nkx;
+    a.nblk = p.Pc * nkb_;  // gathered blocks (c, b) in global kx order
+    for (int c = 0; c < p.Pc; ++c)
+      for (int b = 0; b < nkb_; ++b) a.kx_start[c * nkb_ + b] = kb_gstart(c, b);
+    a.kx_start[a.nblk] = p.nkx;
     for (int f = 0; f < 2; ++f)
-      kz0_symmetrize_dist(field_ptr(f == 0 ? PHI : OMEGA), col_all + f * all * esz_, a, fp64_, s_comp_);
+      for (int b = 0; b < nkb_; ++b) {
+        a.nkx_loc = kb_cnt_[b];
+        a.kx0 = p.kx0 + kb_start_[b];
+        kz0_symmetrize_dist(static_cast<char*>(field_ptr(f == 0 ? PHI : OMEGA)) + kb_off_[b] * esz_,
+                            col_all + f * all * esz_, a, fp64_, s_comp_);
+      }
   }
   prepared_ = false;
 }
@@ -1648,7 +1775,7 @@ void Solver::rollback() {
 
 void Solver::inject_nan(int f) {
   // an interior point of line 1 of the field (line 0 on the owner rank holds U)
-  const size_t elem = static_cast<size_t>(plan_.NY / 2) * plan_.lines_loc() + std::min(1, plan_.lines_loc() - 1);
+  const size_t elem = kb_index(plan_.NY / 2, 0, 0) + std::min(1, plan_.lines_loc() - 1);
   ::channel::inject_nan(field_ptr(f), elem, fp64_, s_comp_);
   HIP_CHECK(hipStreamSynchronize(s_comp_));
 }
@@ -1689,7 +1816,17 @@ Solver::Spectra Solver::spectra() {
   a.ekx = ekx;
   a.ekz = ekz;
   a.map = map;
-  spectra_accumulate(a, fp64_, s_comp_);
+  for (int b = 0; b < nkb_; ++b) {  // per kx sub-block (accumulating; map rows are disjoint)
+    SpectraArgs ab = a;
+    const size_t off = kb_off_[b] * esz_;
+    ab.u = static_cast<const char*>(a.u) + off;
+    ab.v = static_cast<const char*>(a.v) + off;
+    ab.w = static_cast<const char*>(a.w) + off;
+    ab.lines = kb_cnt_[b] * p.nkz_loc;
+    ab.nkx_loc = kb_cnt_[b];
+    ab.kx0 = p.kx0 + kb_start_[b];
+    spectra_accumulate(ab, fp64_, s_comp_);
+  }
   if (comm_) {
     HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_stats_, 0));

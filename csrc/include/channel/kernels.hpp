@@ -99,14 +99,16 @@ struct Twiddles {
 };
 // Source of a spectral field for the backward x-transform: for P ranks the blocks received from
 // each source rank s hold [y_local][nkx_s][nkz] starting at element offset off[s].
-// Block self_seg (this rank's own kx range, if >= 0) lives at self_base + f * self_field_stride
-// + off[self_seg] instead (the spectral field itself: no self exchange, no copy).
+// Blocks self_seg .. self_seg + nself - 1 (this rank's own kx range, if self_seg >= 0; several when
+// the rank's spectral fields are stored as kx sub-blocks, Solver::nkb_) live at self_base + f *
+// self_field_stride + off[s] instead (the spectral field itself: no self exchange, no copy).
 struct XSrc {
   const void* base = nullptr;
   int nsrc = 1;
   int kx_start[9] = {0};   // global retained-kx start of source s (kx_start[nsrc] = nkx)
   long long off[8] = {0};  // element offset of source block s
   int self_seg = -1;
+  int nself = 1;
   const void* self_base = nullptr;
   long long self_field_stride = 0;
 };
@@ -116,6 +118,7 @@ struct XDst {             // destination blocks for the forward x-transform (per
   int kx_start[9] = {0};
   long long off[8] = {0};
   int self_seg = -1;
+  int nself = 1;
   void* self_base = nullptr;
   long long self_field_stride = 0;
 };

@@ -128,6 +128,8 @@ class Solver {
   void* field_ptr(int f) const;
   void* phys_ptr() const { return phys_; }
   const YTablesDev& ytables() const { return ytab_; }
+  // kx sub-blocks of the local spectral layout (1 = plain [y][kx_local][kz]; see nkb_)
+  int kblocks() const { return nkb_; }
   void substep_debug(int n);            // one substep, eager (tests)
   void transforms_debug(bool dt_update);  // backward + phys + forward only (tests)
   Comm* comm() { return comm_.get(); }
@@ -151,6 +153,8 @@ class Solver {
   // exchange of y chunk k (rows [k*ch, (k+1)*ch) of every rank's y range) for nf fields over the
   // column group (the world for the slab)
   void a2a_slab_chunk(int k, int ch, bool to_phys, int nf);
+  // the same for rows [r0, r0 + nr) of every rank's y range and kx sub-blocks [blo, bhi) only
+  void a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bhi);
   // pencil: the same y-chunked pipeline with the B exchange (row group, x <-> kz) between the x
   // transforms and the z stage
   void transforms_pencil(int n, const XArgs& xa, const ZArgs& za, const DtArgs& da);
@@ -222,6 +226,19 @@ class Solver {
   std::vector<hipEvent_t> ev_pen_[6];
   int ychunk_p_ = 0;                       // y planes per chunk of the P > 1 slab pipeline
   bool self_direct_ = true;                // slab: own kx block read/written in place (no self copy)
+  // K-SPEC / exchange overlap (P > 1 slab, and a 1-rank communicator): the local spectral fields
+  // are stored as nkb_ kx sub-blocks, each [y][kx in block][kz] (block b at element kb_off_[b] of
+  // every field).  K-SPEC runs block by block and the backward exchange of block b goes out on the
+  // comm stream while block b+1 is solved.  Every rank splits its
+  // kx range the same way (balanced), so block (c, b) of rank c is one exchange segment of the x
+  // transforms (Pc * nkb_ <= 8 segments).
+  int nkb_ = 1;
+  std::vector<int> kb_start_, kb_cnt_;     // local ikx start / count of block b (this rank)
+  std::vector<size_t> kb_off_;             // element offset of block b in a spectral field
+  std::vector<hipEvent_t> ev_kb_;          // K-SPEC block b done (compute stream)
+  int kb_gstart(int c, int b) const;       // global retained-kx start of block b of column rank c
+  int kb_gcount(int c, int b) const;
+  size_t kb_index(int y, int ikx, int kz) const;  // blocked element index of (y, local kx, kz)
   // phase timing: event pool and the (phase, start, end) pairs of the current step
   struct TPair {
     int phase;
