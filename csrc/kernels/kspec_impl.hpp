@@ -41,6 +41,16 @@ namespace channel {
 
 using namespace dev;
 
+// async global->LDS staging of the inputs where it applies (R > 8 with two tiles); compile with
+// -DCH_KSPEC_GLDS=0 for the address-only A/B
+constexpr bool kspec_glds_enabled() {
+#if defined(CH_KSPEC_GLDS) && CH_KSPEC_GLDS == 0
+  return false;
+#else
+  return true;
+#endif
+}
+
 // ------------------------------------------------------------------------------------------
 // Staging of W lines through an LDS tile (double-buffered where tile2 is set) with NS register
 // prefetch slots (or address-only slots where registers are short: R > 8).
@@ -49,7 +59,15 @@ using namespace dev;
 // 8-B words, which spreads the 32 lanes of each ds_read_b64 half over all 64 banks; G = 1 fixes
 // the parity for even R.  Thread t of the cooperative copies handles rows t/W + 64 q of line t%W,
 // so both the LDS and the global addresses are one base plus compile-time / scalar offsets.
-template <int R, typename T, int W, int NS>
+//
+// R > 8 (the VGPR cap leaves no room for register slots) with two tiles: the prefetch is an
+// asynchronous global->LDS copy (global_load_lds_dword, no VGPRs) of the W lines' rows into the
+// spare tile in their global order [y][W lines] (8 lanes per row, one dword each: the rows start
+// at 8-byte boundaries only, lines = nkx_loc * nkz may be odd); commit() waits for it and reads
+// the column from that raw image (4-way LDS bank conflicts on the column read, against an HBM
+// round trip per field that the address-only slots exposed: 60 % of the R = 10 kernel's cycles
+// sat in the input phases).  The last, partial tile of the grid keeps the address-only path.
+template <int R, typename T, int W, int NS, bool GL = false>
 struct Stage {
   using T2 = typename Cplx<T>::type;
   static constexpr int PITCH = W + 1;
@@ -57,6 +75,10 @@ struct Stage {
   static constexpr int TILE = 64 * R * PITCH + (G ? 64 : 0);
   static constexpr int RPB = 64;  // rows per copy pass: W * 64 threads / W lines
   static constexpr bool kRegSlots = R <= 8;
+  static constexpr int DPE = static_cast<int>(sizeof(T2)) / 4;  // dwords per element
+  static constexpr int DPR = W * DPE;                             // dwords per raw row
+  static constexpr bool kGldsOk = !kRegSlots && 64 % DPR == 0;
+  static_assert(!GL || (kGldsOk && kspec_glds_enabled()), "async LDS staging needs R > 8 and 64 % (W * dwords) == 0");
   T2* tile;   // buffer of the last staging (column() reads it)
   T2* tile2;  // the other buffer (nullptr: single-buffered)
   int N, lines, line0, w, lane;
@@ -66,8 +88,8 @@ struct Stage {
   // hoisted out of the tile loop into ~2 registers per field
   unsigned toff = 0, pstride = 0;
   T2 pend[kRegSlots ? NS : 1][R];
-  const T2* dsrc[kRegSlots ? 1 : NS];
-  unsigned doff[kRegSlots ? 1 : NS];
+  const T2* dsrc[kRegSlots || GL ? 1 : NS];
+  unsigned doff[kRegSlots || GL ? 1 : NS];
 
   static __device__ __forceinline__ int row_off(int y) { return y * PITCH + (G ? (y / R) : 0); }
   __device__ __forceinline__ unsigned thread_off(int l0) const {
@@ -96,7 +118,26 @@ struct Stage {
   template <int S>
   __device__ __forceinline__ void prefetch_at(const T2* __restrict__ src, int l0) {
     const unsigned o = thread_off(l0);
-    if constexpr (!kRegSlots) {
+    if constexpr (GL) {
+      // rows y = RPI k + lane / DPR, dword lane % DPR of the row (line l0 + dw / DPE clamped to the
+      // last line: lines >= lines are staged but never stored); instruction k (wave k % W) writes
+      // LDS dwords 64 k .. 64 k + 63 of the spare tile
+      constexpr int RPI = 64 / DPR;  // rows per instruction
+      const int lane = __lane_id();
+      const int ry = lane / DPR, dw = lane % DPR;
+      const unsigned stride = static_cast<unsigned>(lines) * DPE;  // dwords per global row
+      const unsigned base = static_cast<unsigned>(min(l0 + dw / DPE, lines - 1)) * DPE + dw % DPE;
+      const unsigned* srcd = reinterpret_cast<const unsigned*>(src);
+      unsigned* dstd = reinterpret_cast<unsigned*>(tile2);
+      const int ninst = (N + RPI - 1) / RPI;
+      for (int k = w; k < ninst; k += W) {
+        const int y = k * RPI + ry;
+        if (y < N)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(srcd + (base + static_cast<unsigned>(y) * stride)),
+                                           (__attribute__((address_space(3))) void*)(dstd + 64 * k), 4, 0, 0);
+      }
+      (void)o;
+    } else if constexpr (!kRegSlots) {
       dsrc[S] = src;
       doff[S] = o;
     } else {
@@ -117,6 +158,19 @@ struct Stage {
   template <int S>
   __device__ __forceinline__ void commit(double (&x)[2][R]) {
     next_tile();
+    if constexpr (GL) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the copy landed
+      lds_barrier();                                   // ... and every other wave's
+      const T2* c = tile + w;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int y = lane * R + r;
+        const T2 v = c[(y < N ? y : 0) * W];  // raw image: rows >= N were never written
+        x[0][r] = y < N ? static_cast<double>(v.x) : 0.0;
+        x[1][r] = y < N ? static_cast<double>(v.y) : 0.0;
+      }
+      return;
+    }
     const int y0 = threadIdx.x / W, l = threadIdx.x % W;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
@@ -222,7 +276,8 @@ constexpr int kParDD = 1, kParAnalytic = 2;
 template <int R, typename T, int W, int NS, int XM, int PAR>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
-  using St = Stage<R, T, W, NS>;
+  constexpr bool kGldsTile = Stage<R, T, W, 1>::kGldsOk && kspec_double_tile<R, T, W>() && kspec_glds_enabled();
+  using St = Stage<R, T, W, NS, kGldsTile>;
   constexpr int ROWS = 64 * R;
   constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
   constexpr int NTAB = kspec_lds_tables_doubles<R, T, W>();
@@ -631,8 +686,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       st.store(phi, ph);
       KSPEC_STAMP(6)
-      // the next tile's first inputs load during the D1 solve and the output stores
-      if (has_next) {
+      // the next tile's first inputs load during the D1 solve and the output stores (the async
+      // LDS copies go out after the output stores instead: those use both tiles)
+      if (!kGldsTile && has_next) {
         ahead(std::integral_constant<int, 0>{}, next_line0);
         if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
       }
@@ -761,6 +817,10 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
     }
     KSPEC_STAMP(9)
+    if (kGldsTile && has_next) {
+      ahead(std::integral_constant<int, 0>{}, next_line0);
+      if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
+    }
   }  // tile loop
 #undef KSPEC_STAMP
 }
