@@ -77,8 +77,8 @@ struct Stage {
   static constexpr bool kRegSlots = R <= 8;
   static constexpr int DPE = static_cast<int>(sizeof(T2)) / 4;  // dwords per element
   static constexpr int DPR = W * DPE;                             // dwords per raw row
-  static constexpr bool kGldsOk = !kRegSlots && 64 % DPR == 0;
-  static_assert(!GL || (kGldsOk && kspec_glds_enabled()), "async LDS staging needs R > 8 and 64 % (W * dwords) == 0");
+  static constexpr bool kGldsOk = 64 % DPR == 0;
+  static_assert(!GL || (kGldsOk && kspec_glds_enabled()), "async LDS staging needs 64 % (W * dwords) == 0");
   T2* tile;   // buffer of the last staging (column() reads it)
   T2* tile2;  // the other buffer (nullptr: single-buffered)
   int N, lines, line0, w, lane;
@@ -273,10 +273,13 @@ constexpr bool kspec_double_tile() {
 // register allocation of the default kernel.
 constexpr int kParDD = 1, kParAnalytic = 2;
 
-template <int R, typename T, int W, int NS, int XM, int PAR>
+// GLM: 0 = async LDS staging where the registers are short (R > 8, two tiles), 1 = also at R <= 8
+// in place of the register slots (one field ahead instead of NS)
+template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
-  constexpr bool kGldsTile = Stage<R, T, W, 1>::kGldsOk && kspec_double_tile<R, T, W>() && kspec_glds_enabled();
+  constexpr bool kGldsTile = (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
+                             kspec_double_tile<R, T, W>() && kspec_glds_enabled();
   using St = Stage<R, T, W, NS, kGldsTile>;
   constexpr int ROWS = 64 * R;
   constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
@@ -366,7 +369,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // input sequence of mode 1: 0 H_x, 1 H_z, 2 H_y, 3 phi, 4 omega, 5 R_phi, 6 R_omega (5, 6 only
   // when the substep uses the previous nonlinear term); input i goes to slot i % NS and is
   // prefetched when input i - NS is committed
-  constexpr int D = NS;
+  constexpr int D = kGldsTile ? 1 : NS;  // (one spare tile: one field ahead)
   const int nin = zprev ? 7 : 5;
   auto src_of = [&](int i) -> const T2* {
     switch (i) {
@@ -825,10 +828,23 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #undef KSPEC_STAMP
 }
 
+// CHANNEL_KSPEC_GLDS7=1: the R = 7 fp32 kernel (headline grid) with async LDS staging instead of
+// its two register slots (A/B)
+static bool kspec_glds7() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_GLDS7");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_lines<R, T>();
   auto kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR>;
+  if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
+    if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
+  }
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;
   dim3 grid(std::min(ntiles, resident_blocks(reinterpret_cast<const void*>(kern), W * 64))), block(W * 64);
