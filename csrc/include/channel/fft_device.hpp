@@ -417,12 +417,25 @@ __device__ __forceinline__ void row_sync() {
 // global<->LDS staging, not per pass.
 // TPR threads (64: one wave; 128: two waves of one block) share the rows; lane = thread index
 // within them
-template <int N, int R, int NS, int RW, int PITCH, bool INV, int TPR = 64, typename T2>
+// Zero band of a 2/3-dealiased spectral row of length N (kx = N/3 + 1 .. N - N/3 - 1 are zero):
+// for the first pass (NS = 1) of an inverse x transform, input block r (elements Q r .. Q r + Q - 1)
+// is entirely in the band when zero_block() holds; those inputs are never read (compile-time zeros,
+// so the DFT drops their terms) and never need to be written
+template <int N, int Q>
+__host__ __device__ constexpr bool zero_block(int r) {
+  return Q * r >= N / 3 + 1 && Q * r + Q - 1 <= N - N / 3 - 1;
+}
+
+template <int N, int R, int NS, int RW, int PITCH, bool INV, int TPR = 64, bool ZB = false, bool TR = false,
+          typename T2>
 __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
-  // tw: this pass's [R-1][NS] twiddle table
+  // tw: this pass's [R-1][NS] twiddle table; ZB: first pass of a zero-band input (zero_block);
+  // TR: last pass of a forward x transform whose outputs in the 2/3-rule band are discarded (not
+  // written back)
   constexpr int Q = N / R;
   constexpr int NB = RW * Q;
   constexpr int B = (NB + TPR - 1) / TPR;
+  static_assert(!ZB || NS == 1, "zero-band pruning applies to the first pass");
   T2 v[B][R];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
@@ -431,7 +444,10 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       const int row = idx / Q, j = idx - row * Q;
       const T2* p = buf + row * PITCH;
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(j + r * Q)];
+      for (int r = 0; r < R; ++r) {
+        if (ZB && zero_block<N, Q>(r)) v[b][r] = T2{0, 0};
+        else v[b][r] = p[fft_pidx(j + r * Q)];
+      }
     }
   }
   row_sync<TPR>();
@@ -451,18 +467,22 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       T2* p = buf + row * PITCH;
       const int base = (j - k) * R + k;
 #pragma unroll
-      for (int r = 0; r < R; ++r) p[fft_pidx(base + r * NS)] = v[b][r];
+      for (int r = 0; r < R; ++r) {
+        const int pos = base + r * NS;
+        if (!TR || pos <= N / 3 || pos >= N - N / 3) p[fft_pidx(pos)] = v[b][r];
+      }
     }
   }
   row_sync<TPR>();
 }
 
-template <int N, int RW, int PITCH, bool INV, int TPR = 64, typename T2>
+template <int N, int RW, int PITCH, bool INV, int TPR = 64, bool ZB = false, bool TR = false, typename T2>
 __device__ __forceinline__ void wave_fft(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
   using Pl = FftPlan<N>;
-  wave_pass<N, Pl::R0, 1, RW, PITCH, INV, TPR>(buf, tw, lane);
-  if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV, TPR>(buf, tw, lane);
-  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV, TPR>(buf, tw + Pl::T1, lane);
+  constexpr bool L0 = Pl::R1 == 1, L1 = Pl::R1 > 1 && Pl::R2 == 1;  // which pass is the last
+  wave_pass<N, Pl::R0, 1, RW, PITCH, INV, TPR, ZB, TR && L0>(buf, tw, lane);
+  if constexpr (Pl::R1 > 1) wave_pass<N, Pl::R1, Pl::R0, RW, PITCH, INV, TPR, false, TR && L1>(buf, tw, lane);
+  if constexpr (Pl::R2 > 1) wave_pass<N, Pl::R2, Pl::R0 * Pl::R1, RW, PITCH, INV, TPR, false, TR>(buf, tw + Pl::T1, lane);
 }
 
 // ---- register-edge passes (one butterfly column per lane: N / R0 == TPR) ------------------------

@@ -72,7 +72,8 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   const XArgs a = norm_pseg(a_in);
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_backward: twiddle table mismatch");
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
-  CH_CHECK(a.nkx <= 2 * (a.NX / 3) + 1, "xfft_backward: more retained kx than the 2/3 rule allows");
+  // the first pass skips the zero band of the 2/3 rule at compile time (wave_pass ZB)
+  CH_CHECK(a.Kx == a.NX / 3 && a.nkx == 2 * a.Kx + 1, "xfft_backward: retained kx must be the 2/3 rule's (Kx = NX/3)");
   CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_backward: per-field plane block exceeds 32-bit offsets");
   CH_DISPATCH_N(a.NX, fft_xb_len<NN>(a, src, phys, tw, fp64, s));

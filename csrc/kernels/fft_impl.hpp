@@ -206,9 +206,18 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         for (int u = 0; u < V; ++u)
           s[(c + u) * PITCH + fft_pidx(x)] = (q == 0 && u == 0 && zmean && e == 0) ? T2{0, 0} : v[q].c[u];
     }
-    for (int e = tid; e < (NX - a.nkx) * C; e += NT) {
-      const int j = e / C, c = e - j * C;
-      s[c * PITCH + fft_pidx(a.Kx + 1 + j)] = T2{0, 0};
+    // zero padding: only the band elements the first pass reads (its input blocks that straddle
+    // the band edges; the blocks inside the band are compile-time zeros, wave_pass ZB)
+    {
+      constexpr int Q0 = NX / FftPlan<NX>::R0, KX = NX / 3;
+      constexpr int ZLO = KX + 1, ZHI = NX - KX - 1;                    // band [ZLO, ZHI]
+      constexpr int E1 = ZLO % Q0 ? std::min(ZHI, Q0 * (ZLO / Q0 + 1) - 1) : ZLO - 1;  // [ZLO, E1]
+      constexpr int S2 = (ZHI + 1) % Q0 ? std::max(ZLO, Q0 * (ZHI / Q0)) : ZHI + 1;    // [S2, ZHI]
+      constexpr int N1 = E1 - ZLO + 1, N2 = (S2 > E1 ? ZHI - S2 + 1 : 0);
+      for (int e = tid; e < (N1 + N2) * C; e += NT) {
+        const int j = e / C, c = e - j * C;
+        s[c * PITCH + fft_pidx(j < N1 ? ZLO + j : S2 + (j - N1))] = T2{0, 0};
+      }
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
@@ -222,7 +231,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       if (!(a.diag & 1))
 #pragma unroll 1
         for (int rr = 0; rr < RW; rr += RB)
-          wave_fft<NX, RB, PITCH, true, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+          wave_fft<NX, RB, PITCH, true, TPR, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
@@ -314,7 +323,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       if (!(a.diag & 1))
 #pragma unroll 1
         for (int rr = 0; rr < RW; rr += RB)
-          wave_fft<NX, RB, PITCH, false, TPR>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
+          wave_fft<NX, RB, PITCH, false, TPR, false, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;

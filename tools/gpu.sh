@@ -13,6 +13,7 @@
 #   configs          bench.py on every BASELINE config that fits one GPU
 #   rehearse2        2-rank torchrun bench on one GPU over the shared-memory loopback data plane
 #   rehearse8        8-rank bench.py --gpus 8 (slab, then pencil 2x4) over the loopback, headline grid
+#   rehearse24       2- and 4-rank bench.py (slab, kx sub-block overlap) over the loopback, headline grid
 #   ab               bench.py once per env setting in AB_ENVS ("A=1 B=2;A=2 B=2")
 #   probe            transform stage alone (tools/xform_probe.py $PROBE_ARGS) per env setting in PROBE_ENVS
 #   kprobe           rocprofv3 kernel stats of the transform stage on one stream (env: $KPROBE_ENV)
@@ -86,6 +87,14 @@ for step in "$@"; do
         CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus 8 --decomposition $dec --steps 2 --warmup 1 \
           $BENCH_ARGS > gpurun_out/${tag}_rehearse8_$dec.log 2>&1 || fail "rehearse8 $dec" gpurun_out/${tag}_rehearse8_$dec.log
         tail -n 1 gpurun_out/${tag}_rehearse8_$dec.log
+      done ;;
+    rehearse24)
+      # 2 and 4 ranks (slab: 4 and 2 kx sub-blocks, the K-SPEC / exchange overlap) on the one GPU
+      # over the shared-memory loopback at the headline shape
+      for n in 2 4; do
+        CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus $n --steps 2 --warmup 1 \
+          $BENCH_ARGS > gpurun_out/${tag}_rehearse$n.log 2>&1 || fail "rehearse $n" gpurun_out/${tag}_rehearse$n.log
+        tail -n 1 gpurun_out/${tag}_rehearse$n.log
       done ;;
     ab)
       IFS=';' read -ra settings <<< "$AB_ENVS"
