@@ -66,7 +66,11 @@ constexpr bool kspec_glds_enabled() {
 // at 8-byte boundaries only, lines = nkx_loc * nkz may be odd); commit() waits for it and reads
 // the column from that raw image (4-way LDS bank conflicts on the column read, against an HBM
 // round trip per field that the address-only slots exposed: 60 % of the R = 10 kernel's cycles
-// sat in the input phases).  The last, partial tile of the grid keeps the address-only path.
+// sat in the input phases).  Lines past the end (the last tile) copy the last line, rows >= N
+// are not copied and read as zero.  One field ahead only (one spare tile), and the next tile's
+// first field goes out after the output stores, which use both tiles; at R <= 8 the register
+// slots (two fields ahead, the next tile's issued during the D1 solve) measured faster
+// (profiles/r03s3/ab_kspec_glds_r7.txt).
 template <int R, typename T, int W, int NS, bool GL = false>
 struct Stage {
   using T2 = typename Cplx<T>::type;
@@ -838,12 +842,22 @@ static bool kspec_glds7() {
   return on;
 }
 
+// CHANNEL_KSPEC_NS7=3: the R = 7 fp32 kernel with three register prefetch slots (A/B)
+static int kspec_ns7() {
+  static const int ns = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_NS7");
+    return e ? std::atoi(e) : 0;
+  }();
+  return ns;
+}
+
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_lines<R, T>();
   auto kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR>;
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
+    if (kspec_ns7() == 3) kern = kspec_kernel<R, T, W, 3, kspec_xmode<R, T>(), PAR>;
   }
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;

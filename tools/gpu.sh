@@ -92,7 +92,7 @@ for step in "$@"; do
       # 2 and 4 ranks (slab: 4 and 2 kx sub-blocks, the K-SPEC / exchange overlap) on the one GPU
       # over the shared-memory loopback at the headline shape
       for n in 2 4; do
-        CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus $n --steps 2 --warmup 1 \
+        CHANNEL_COMM=shm CHANNEL_SHM_SLOT_MB=64 timeout -k 10 600 python bench.py --gpus $n --steps 2 --warmup 1 \
           $BENCH_ARGS > gpurun_out/${tag}_rehearse$n.log 2>&1 || fail "rehearse $n" gpurun_out/${tag}_rehearse$n.log
         tail -n 1 gpurun_out/${tag}_rehearse$n.log
       done ;;
