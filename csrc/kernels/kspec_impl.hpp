@@ -206,6 +206,20 @@ struct Stage {
     prefetch_at<0>(src, line0);
     commit<0>(x);
   }
+  // Direct store (A/B, kspec_kernel DS): each lane writes its own rows of its line straight from
+  // the registers (8-byte scattered stores; the W waves of the block fill adjacent 8-byte words of
+  // each row), no LDS transpose and no block barrier
+  __device__ __forceinline__ void store_direct(T2* __restrict__ dst, const double (&re)[R], const double (&im)[R],
+                                               double sc = 1.0) {
+    if (line0 + w < lines) {
+      T2* d = dst + line0 + w;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = lane * R + r;
+        if (j < N) d[static_cast<unsigned>(j) * static_cast<unsigned>(lines)] = T2{static_cast<T>(sc * re[r]), static_cast<T>(sc * im[r])};
+      }
+    }
+  }
   // rows >= N are written too: the operators keep them at exactly zero
   __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&x)[2][R]) { store(dst, x[0], x[1]); }
   // (re, im) rows of a line, optionally scaled (wave-uniform)
@@ -279,7 +293,9 @@ constexpr int kParDD = 1, kParAnalytic = 2;
 
 // GLM: 0 = async LDS staging where the registers are short (R > 8, two tiles), 1 = also at R <= 8
 // in place of the register slots (one field ahead instead of NS)
-template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0>
+// DS = 1: every store except omega's (re-read from its tile) goes straight from the registers
+// (Stage::store_direct; A/B)
+template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0, int DS = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
   constexpr bool kGldsTile = (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
@@ -356,7 +372,10 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // statistics reduction [4][64 R] in the staging tiles: between the phi store and the output
   // stores nothing reads them, and the output stores rewrite every slot a column read uses
   // (padding rows included, with zeros) before the next staging
-  double* sred = reinterpret_cast<double*>(tile_mem);
+  // (DS: the tiles' padding rows must stay zero for the column reads, so the reduction gets its own
+  // LDS: no tile store rewrites them afterwards)
+  __shared__ double sred_own[DS ? 4 * ROWS : 1];
+  double* sred = DS ? sred_own : reinterpret_cast<double*>(tile_mem);
   static_assert(St::TILE * sizeof(T2) >= 4 * ROWS * sizeof(double), "tile too small for the statistics reduction");
 
   // Persistent blocks: the grid is the resident capacity and each block walks tiles of W lines.
@@ -374,6 +393,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // when the substep uses the previous nonlinear term); input i goes to slot i % NS and is
   // prefetched when input i - NS is committed
   constexpr int D = kGldsTile ? 1 : NS;  // (one spare tile: one field ahead)
+  static_assert(D >= 1 && D <= 3, "prefetch distance: the first D inputs of a tile are issued explicitly");
   const int nin = zprev ? 7 : 5;
   auto src_of = [&](int i) -> const T2* {
     switch (i) {
@@ -395,6 +415,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   if (a.mode == 1 && lb < ntiles) {
     ahead(std::integral_constant<int, 0>{}, lb * W);
     if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, lb * W);
+    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, lb * W);
   }
   // optional per-phase shader-clock accounting (CHANNEL_KSPEC_PROF)
   const bool prof_on = a.prof != nullptr;
@@ -533,8 +554,13 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       KSPEC_STAMP(1)
       if (a.store_r) {  // (the last substep's R is never read: the next substep has zeta = 0)
-        st.store(Rphi, RPn);
-        st.store(Romega, RWn);
+        if constexpr (DS) {
+          st.store_direct(Rphi, RPn[0], RPn[1]);
+          st.store_direct(Romega, RWn[0], RWn[1]);
+        } else {
+          st.store(Rphi, RPn);
+          st.store(Romega, RWn);
+        }
       }
       KSPEC_STAMP(2)
 
@@ -691,13 +717,15 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           vo[3][r] = om[1][r];
         }
       }
-      st.store(phi, ph);
+      if constexpr (DS) st.store_direct(phi, ph[0], ph[1]);
+      else st.store(phi, ph);
       KSPEC_STAMP(6)
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
       if (!kGldsTile && has_next) {
         ahead(std::integral_constant<int, 0>{}, next_line0);
         if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
+    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
       }
     } else {
       // ---------------- prepare only: fields from the state --------------------------------
@@ -777,18 +805,22 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       __syncthreads();  // sred is a staging tile again
     }
     KSPEC_STAMP(8)
-    st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);  // v
+    auto ostore = [&](void* dst, const double (&re)[R], const double (&im)[R], double sc = 1.0) {
+      if constexpr (DS) st.store_direct(static_cast<T2*>(dst), re, im, sc);
+      else st.store(static_cast<T2*>(dst), re, im, sc);
+    };
+    ostore(a.out[1], vo[0], vo[1]);  // v
     // omega_y: when out[4] is the omega state itself (the solver's layout) it is already stored;
     // the x transform reads its mean line (U) as 0
-    if (a.out[4] != a.omega) st.store(static_cast<T2*>(a.out[4]), vo[2], vo[3], 1.0 - mf);
+    if (a.out[4] != a.omega) ostore(a.out[4], vo[2], vo[3], 1.0 - mf);
     {
       double x[2][R];
 #pragma unroll
       for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
-      st.store(static_cast<T2*>(a.out[0]), x);
+      ostore(a.out[0], x[0], x[1]);
 #pragma unroll
       for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
-      st.store(static_cast<T2*>(a.out[2]), x);
+      ostore(a.out[2], x[0], x[1]);
       // vorticity: wx = Dw - i be v ; wz = i al v - Du   (convolution_kernels.cu:46-53)
       // D(dv) = D2 v = phi + k2 v (Helmholtz identity, consistent with the compact D2 operator)
 #pragma unroll
@@ -798,7 +830,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         x[0][r] = -bi + be * vo[1][r];
         x[1][r] = br - be * vo[0][r];
       }
-      st.store(static_cast<T2*>(a.out[3]), x);
+      ostore(a.out[3], x[0], x[1]);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
@@ -807,7 +839,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         x[0][r] = -al * vo[1][r] + ai - mf * dvo[2][r];
         x[1][r] = al * vo[0][r] - ar;
       }
-      st.store(static_cast<T2*>(a.out[5]), x);
+      ostore(a.out[5], x[0], x[1]);
     }
     if (a.mean_diag && is_mean) {
       const double d0 = row_value<R, XM>(dvo[2], 0, lane), dN = row_value<R, XM>(dvo[2], N - 1, lane);
@@ -827,6 +859,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     if (kGldsTile && has_next) {
       ahead(std::integral_constant<int, 0>{}, next_line0);
       if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
+    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
     }
   }  // tile loop
 #undef KSPEC_STAMP
@@ -852,6 +885,15 @@ static int kspec_ns7() {
   return ns;
 }
 
+// CHANNEL_KSPEC_DSTORE7=1: the R = 7 fp32 kernel with direct (register -> global) stores (A/B)
+static bool kspec_dstore7() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_DSTORE7");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_lines<R, T>();
@@ -859,6 +901,7 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
     if (kspec_ns7() == 2) kern = kspec_kernel<R, T, W, 2, kspec_xmode<R, T>(), PAR>;
+    if (kspec_dstore7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 0, 1>;
   }
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;
