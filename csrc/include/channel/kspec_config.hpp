@@ -32,12 +32,11 @@ constexpr int kspec_xmode() {
   return R <= 12 ? dev::kXlLds : dev::kXlDpp;
 }
 
-// register prefetch slots for the input fields (prefetch distance); R = 7 fp32 (the headline
-// grid) takes three: 424 registers instead of 436 and 37.25 vs 37.76 ms/step (A/B,
-// profiles/r03s3/ab_kspec_ns7.txt)
+// register prefetch slots for the input fields (prefetch distance); three at R = 7 measured the
+// same as two (profiles/r03s3/ab_kspec_ns7.txt)
 template <int R, typename T>
 constexpr int kspec_slots() {
-  return R <= 4 ? 1 : (R == 7 && sizeof(T) == 4 ? 3 : (R <= 8 ? 2 : 1));
+  return R <= 4 ? 1 : (R <= 8 ? 2 : 1);
 }
 
 // dispatch a runtime R to the instantiated rows-per-lane values

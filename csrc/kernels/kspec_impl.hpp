@@ -875,8 +875,7 @@ static bool kspec_glds7() {
   return on;
 }
 
-// CHANNEL_KSPEC_NS7=2: the R = 7 fp32 kernel with two register prefetch slots (the round-3 A/B
-// baseline; the default is three)
+// CHANNEL_KSPEC_NS7=3: the R = 7 fp32 kernel with three register prefetch slots (A/B)
 static int kspec_ns7() {
   static const int ns = [] {
     const char* e = std::getenv("CHANNEL_KSPEC_NS7");
@@ -900,7 +899,7 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   auto kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR>;
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
-    if (kspec_ns7() == 2) kern = kspec_kernel<R, T, W, 2, kspec_xmode<R, T>(), PAR>;
+    if (kspec_ns7() == 3) kern = kspec_kernel<R, T, W, 3, kspec_xmode<R, T>(), PAR>;
     if (kspec_dstore7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 0, 1>;
   }
   // persistent grid: as many blocks as can be resident at once
