@@ -206,20 +206,6 @@ struct Stage {
     prefetch_at<0>(src, line0);
     commit<0>(x);
   }
-  // Direct store (A/B, kspec_kernel DS): each lane writes its own rows of its line straight from
-  // the registers (8-byte scattered stores; the W waves of the block fill adjacent 8-byte words of
-  // each row), no LDS transpose and no block barrier
-  __device__ __forceinline__ void store_direct(T2* __restrict__ dst, const double (&re)[R], const double (&im)[R],
-                                               double sc = 1.0) {
-    if (line0 + w < lines) {
-      T2* d = dst + line0 + w;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int j = lane * R + r;
-        if (j < N) d[static_cast<unsigned>(j) * static_cast<unsigned>(lines)] = T2{static_cast<T>(sc * re[r]), static_cast<T>(sc * im[r])};
-      }
-    }
-  }
   // rows >= N are written too: the operators keep them at exactly zero
   __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&x)[2][R]) { store(dst, x[0], x[1]); }
   // (re, im) rows of a line, optionally scaled (wave-uniform)
@@ -293,9 +279,9 @@ constexpr int kParDD = 1, kParAnalytic = 2;
 
 // GLM: 0 = async LDS staging where the registers are short (R > 8, two tiles), 1 = also at R <= 8
 // in place of the register slots (one field ahead instead of NS)
-// DS = 1: every store except omega's (re-read from its tile) goes straight from the registers
-// (Stage::store_direct; A/B)
-template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0, int DS = 0>
+// (A/B record, not kept: direct register->global stores instead of the tile transposes, 9 % slower
+// at R = 7, profiles/r03s3/ab_kspec_ns7.txt)
+template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
   constexpr bool kGldsTile = (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
@@ -372,10 +358,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   // statistics reduction [4][64 R] in the staging tiles: between the phi store and the output
   // stores nothing reads them, and the output stores rewrite every slot a column read uses
   // (padding rows included, with zeros) before the next staging
-  // (DS: the tiles' padding rows must stay zero for the column reads, so the reduction gets its own
-  // LDS: no tile store rewrites them afterwards)
-  __shared__ double sred_own[DS ? 4 * ROWS : 1];
-  double* sred = DS ? sred_own : reinterpret_cast<double*>(tile_mem);
+  double* sred = reinterpret_cast<double*>(tile_mem);
   static_assert(St::TILE * sizeof(T2) >= 4 * ROWS * sizeof(double), "tile too small for the statistics reduction");
 
   // Persistent blocks: the grid is the resident capacity and each block walks tiles of W lines.
@@ -554,13 +537,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       }
       KSPEC_STAMP(1)
       if (a.store_r) {  // (the last substep's R is never read: the next substep has zeta = 0)
-        if constexpr (DS) {
-          st.store_direct(Rphi, RPn[0], RPn[1]);
-          st.store_direct(Romega, RWn[0], RWn[1]);
-        } else {
-          st.store(Rphi, RPn);
-          st.store(Romega, RWn);
-        }
+        st.store(Rphi, RPn);
+        st.store(Romega, RWn);
       }
       KSPEC_STAMP(2)
 
@@ -717,8 +695,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           vo[3][r] = om[1][r];
         }
       }
-      if constexpr (DS) st.store_direct(phi, ph[0], ph[1]);
-      else st.store(phi, ph);
+      st.store(phi, ph);
       KSPEC_STAMP(6)
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
@@ -806,8 +783,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     }
     KSPEC_STAMP(8)
     auto ostore = [&](void* dst, const double (&re)[R], const double (&im)[R], double sc = 1.0) {
-      if constexpr (DS) st.store_direct(static_cast<T2*>(dst), re, im, sc);
-      else st.store(static_cast<T2*>(dst), re, im, sc);
+      st.store(static_cast<T2*>(dst), re, im, sc);
     };
     ostore(a.out[1], vo[0], vo[1]);  // v
     // omega_y: when out[4] is the omega state itself (the solver's layout) it is already stored;
@@ -884,15 +860,6 @@ static int kspec_ns7() {
   return ns;
 }
 
-// CHANNEL_KSPEC_DSTORE7=1: the R = 7 fp32 kernel with direct (register -> global) stores (A/B)
-static bool kspec_dstore7() {
-  static const bool on = [] {
-    const char* e = std::getenv("CHANNEL_KSPEC_DSTORE7");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
   constexpr int W = kspec_lines<R, T>();
@@ -900,7 +867,6 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
     if (kspec_ns7() == 3) kern = kspec_kernel<R, T, W, 3, kspec_xmode<R, T>(), PAR>;
-    if (kspec_dstore7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 0, 1>;
   }
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;
