@@ -1030,7 +1030,9 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   // its K-SPEC belongs to the previous step (another graph launch), whose events this step's
   // capture cannot wait on.
   const bool overlap = NB > 1 && n > 0;
-  const int bchunk = overlap ? NB - 1 : 0;  // blocks still to send per chunk: [bchunk, NB)
+  const bool present = NB > 1 && n == 0 && presend_done_;  // blocks 0 .. NB-2 already sent
+  presend_done_ = false;
+  const int bchunk = (overlap || present) ? NB - 1 : 0;  // blocks still to send per chunk: [bchunk, NB)
   if (overlap) {
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
@@ -1280,6 +1282,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
 }
 
 void Solver::prepare() {
+  presend_done_ = false;  // the outputs are recomputed: a pre-sent exchange is stale
   kspec(0, 0, cfg_.stats_every > 0);
   stats_pending_ = cfg_.stats_every > 0;
   prepared_ = true;
@@ -1290,6 +1293,29 @@ void Solver::step_body(bool stats) {
     transforms(n, false);
     kspec(1, n, stats && n == 2);
   }
+  // the next step's substep-0 backward exchange of blocks 0 .. NB-2, behind this step's last
+  // K-SPEC blocks (joined back into the compute stream: a captured graph must end there)
+  if (kb_overlap()) presend_backward(true);
+}
+
+// Backward exchange of kx sub-blocks 0 .. nkb_-2 (all rows) for the coming substep 0.
+// wait_blocks: each waits for its K-SPEC block (ev_kb_); otherwise for everything queued on the
+// compute stream so far.  The comm stream is joined back into the compute stream.
+void Solver::presend_backward(bool wait_blocks) {
+  const int maxrows = plan_.y_split.max_count();
+  if (!wait_blocks) {
+    HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  }
+  for (int b = 0; b + 1 < nkb_; ++b) {
+    if (wait_blocks) HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
+    ev(4, false, s_comm_);
+    a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+    ev(4, true, s_comm_);
+  }
+  HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
+  presend_done_ = true;
 }
 
 void Solver::step(bool stats_for_next) {
@@ -1305,6 +1331,8 @@ void Solver::step(bool stats_for_next) {
     }
     HIP_CHECK(hipEventRecord(step_ev_[step_ev_used_].first, s_comp_));
   }
+  // substep 0 relies on blocks 0 .. NB-2 having been sent (the previous step's tail does it)
+  if (kb_overlap() && !presend_done_) presend_backward(false);
   // P > 1: the first step runs eagerly so RCCL connects its peers outside stream capture
   const bool warm = !comm_ || comm_warm_;
   if (use_graph_ && warm && !debug_sync_enabled() && !phase_timing_) {
@@ -1774,6 +1802,7 @@ void Solver::rollback() {
 }
 
 void Solver::inject_nan(int f) {
+  presend_done_ = false;
   // an interior point of line 1 of the field (line 0 on the owner rank holds U)
   const size_t elem = kb_index(plan_.NY / 2, 0, 0) + std::min(1, plan_.lines_loc() - 1);
   ::channel::inject_nan(field_ptr(f), elem, fp64_, s_comp_);

@@ -236,6 +236,13 @@ class Solver {
   std::vector<int> kb_start_, kb_cnt_;     // local ikx start / count of block b (this rank)
   std::vector<size_t> kb_off_;             // element offset of block b in a spectral field
   std::vector<hipEvent_t> ev_kb_;          // K-SPEC block b done (compute stream)
+  // Substep 0 of a step consumes a pre-send: the backward exchange of blocks 0 .. nkb_-2 of the
+  // state's outputs goes out at the end of the previous step (behind the last K-SPEC's blocks,
+  // inside its graph) or, after anything that recomputed the outputs (prepare()), eagerly before
+  // the step.  presend_done_: that exchange has been issued for the next substep 0.
+  bool presend_done_ = false;
+  bool kb_overlap() const { return nkb_ > 1 && comm_ && !plan_.pencil(); }
+  void presend_backward(bool wait_blocks);
   int kb_gstart(int c, int b) const;       // global retained-kx start of block b of column rank c
   int kb_gcount(int c, int b) const;
   size_t kb_index(int y, int ikx, int kz) const;  // blocked element index of (y, local kx, kz)

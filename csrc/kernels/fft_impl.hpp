@@ -447,7 +447,7 @@ constexpr int zphys_rows() {
 }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
-          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 2, int ZPF = 0>
+          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 2>
 __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -520,16 +520,11 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   constexpr bool kRegEdge = TPR == 64 && EP == 16 && FftPlan<NZP>::R0 == 16 && FftPlan<NZP>::R2 > 1 &&
                             fft_reg_edges_ok<NZP, 64>() && 2 * MK <= 16;
   T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
-  // ZPF = 1 (A/B, register-edge path): a second buffer for pair 1, so pair 2 is issued two
-  // transforms ahead (at pair 0) and the next row's pair 1 a whole row ahead (at pair 1)
-  constexpr bool kPF2 = ZPF == 1 && kPrefetch && kRegEdge;
-  T2 qa[kPF2 ? MK : 1], qb[kPF2 ? MK : 1];
+  // (not kept: a second buffer issuing pair 2 two transforms ahead and the next row's pair 1 a
+  // row ahead: 28 spilled VGPRs, 39.4 vs 37.7 ms/step, profiles/r03s3/ab_zphys_prefetch2.txt)
   long long g = blockIdx.x;
   if constexpr (kPrefetch) {
     if (g < ngroups) fetch(g * ZWT + w, 0, pa, pb);
-    if constexpr (kPF2) {
-      if (g < ngroups) fetch(g * ZWT + w, 1, qa, qb);
-    }
   }
   // Rows past the end (TPR < 64 only: the host checks nrows % ZWT == 0 otherwise) run the
   // transforms on zeros and skip every global access.  The loop is block-uniform.
@@ -558,8 +553,8 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       if constexpr (kPrefetch) {
 #pragma unroll
         for (int i = 0; i < MK; ++i) {
-          va[i] = (kPF2 && p == 1) ? qa[i] : pa[i];
-          vb[i] = (kPF2 && p == 1) ? qb[i] : pb[i];
+          va[i] = pa[i];
+          vb[i] = pb[i];
         }
       } else {
         fetch(r, p, va, vb);
@@ -580,10 +575,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           d[i] = ok ? (k == 0 ? T2{va[i].x, vb[i].x} : T2{va[i].x - vb[i].y, va[i].y + vb[i].x}) : T2{0, 0};
           m[i] = ok && k > 0 ? T2{va[i].x + vb[i].y, vb[i].x - va[i].y} : T2{0, 0};
         }
-        if constexpr (kPF2) {
-          if (p == 0) fetch(r, 2, pa, pb);
-          if (p == 1 && more) fetch(rnext, 1, qa, qb);
-        } else if constexpr (kPrefetch) {
+        if constexpr (kPrefetch) {
           if (p < 2) fetch(r, p + 1, pa, pb);
         }
         const int src = (64 - t) & 63;
@@ -1057,15 +1049,6 @@ inline bool zpers_enabled() {
   return on;
 }
 
-// CHANNEL_ZPF=1: the 1024-point fp32 register-edge z stage with two prefetch buffers (A/B)
-inline bool zpf_env() {
-  static const bool on = [] {
-    const char* e = std::getenv("CHANNEL_ZPF");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
-}
-
 template <int NN, typename T, int TPR, int WPE = 2>
 static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, hipStream_t s, bool zh) {
   using T2 = typename C2<T>::type;
@@ -1073,9 +1056,6 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
                          : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
-  if constexpr (NN == 1024 && sizeof(T) == 4 && TPR == 64 && WPE == 2) {
-    if (zpf_env() && a.nseg == 1 && zh) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 1>;
-  }
   const long long ngroups = (nrows + ZR - 1) / ZR;
   const long long cap = zpers_enabled() ? persist_blocks(reinterpret_cast<const void*>(kern), ZR * TPR, "CHANNEL_Z_BPC") : ngroups;
   dim3 grid(static_cast<unsigned>(std::min(ngroups, cap)));
