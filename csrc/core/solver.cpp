@@ -174,12 +174,14 @@ void Solver::alloc() {
   // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
   // every rank (a function of Pc and the environment), at most 8 exchange segments in total
   nkb_ = 1;
-  if (comm_ && !p.pencil()) {
+  if (comm_) {  // (pencil: the column group's A exchange, kx <-> y, is the slab's)
     int want = p.Pc <= 2 ? 4 : (p.Pc <= 4 ? 2 : 1);
     if (const char* e = std::getenv("CHANNEL_KBLOCKS")) want = std::atoi(e);
     int minc = p.nkx;
     for (int c = 0; c < p.Pc; ++c) minc = std::min(minc, p.kx_split.count[c]);
     nkb_ = std::max(1, std::min({want, 8 / p.Pc, minc}));
+    // the round-1 per-field pencil exchange (A/B) addresses whole rank blocks
+    if (p.pencil() && std::getenv("CHANNEL_PENCIL_UNCHUNKED")) nkb_ = 1;
   }
   {
     const Split kb = Split::balanced(p.nkx_loc, nkb_);
@@ -1169,16 +1171,21 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
   xa.npseg = Pr;
   for (int r = 0; r < Pr; ++r) xa.x_start[r] = p.x_split.start[r];
   xa.x_start[Pr] = p.NX;
+  // A-exchange segments: kx sub-block b of column c is segment c * nkb_ + b (global kx order)
+  const int NB = nkb_, NSG = Pc * NB;
+  CH_CHECK(NSG <= 8, "at most 8 exchange segments");
   XSrc src;
   src.base = xbuf_;
-  src.nsrc = Pc;
+  src.nsrc = NSG;
   XDst dst;
   dst.base = xbuf_;
-  dst.ndst = Pc;
-  for (int c = 0; c < Pc; ++c) src.kx_start[c] = dst.kx_start[c] = p.kx_split.start[c];
-  src.kx_start[Pc] = dst.kx_start[Pc] = p.nkx;
-  if (self_direct_) {  // own column block: straight from / into the spectral fields
-    src.self_seg = dst.self_seg = p.pcol;
+  dst.ndst = NSG;
+  for (int c = 0; c < Pc; ++c)
+    for (int b = 0; b < NB; ++b) src.kx_start[c * NB + b] = dst.kx_start[c * NB + b] = kb_gstart(c, b);
+  src.kx_start[NSG] = dst.kx_start[NSG] = p.nkx;
+  if (self_direct_) {  // own column blocks: straight from / into the spectral fields
+    src.self_seg = dst.self_seg = p.pcol * NB;
+    src.nself = dst.nself = NB;
     src.self_base = out_;
     dst.self_base = out_;
     src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
@@ -1198,8 +1205,13 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     for (int r = 0; r < Pr; ++r)
       x.poff[r] = (static_cast<long long>(p.ny_loc) * p.x_split.start[r] + y0 * p.x_split.count[r]) * p.nkz_loc;
     for (int c = 0; c < Pc; ++c)
-      sc.off[c] = dc.off[c] = (static_cast<long long>(p.ny_loc) * p.kx_split.start[c] + y0 * p.kx_split.count[c]) * p.nkz_loc;
-    if (self_direct_) sc.off[p.pcol] = dc.off[p.pcol] = (static_cast<long long>(p.y0) + y0) * p.lines_loc();
+      for (int b = 0; b < NB; ++b)
+        sc.off[c * NB + b] = dc.off[c * NB + b] =
+            (static_cast<long long>(p.ny_loc) * kb_gstart(c, b) + y0 * kb_gcount(c, b)) * p.nkz_loc;
+    if (self_direct_)
+      for (int b = 0; b < NB; ++b)
+        sc.off[p.pcol * NB + b] = dc.off[p.pcol * NB + b] =
+            static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * p.nkz_loc;
   };
   auto xbw = [&](int k) {
     if (chunk_rows(k) > 0) {
@@ -1250,10 +1262,25 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
   };
 
   roctxRangePushA("xzx_pencil_chunked");
-  HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
-  HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  // K-SPEC / A-exchange overlap over kx sub-blocks, as in transforms_slab
+  const bool overlap = NB > 1 && n > 0;
+  const bool present = NB > 1 && n == 0 && presend_done_;
+  presend_done_ = false;
+  const int bchunk = (overlap || present) ? NB - 1 : 0;
+  if (overlap) {
+    for (int b = 0; b + 1 < NB; ++b) {
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
+      ev(4, false, s_comm_);
+      a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+      ev(4, true, s_comm_);
+    }
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
+  } else {
+    HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
+  }
   for (int t = 0; t < nch + 6; ++t) {
-    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_chunk(t, ch, true, 6); });
+    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_rows(t * ch, ch, true, 6, bchunk, NB); });
     if (t - 2 >= 0 && t - 2 < nch) comm_op(t - 2, E_XB, E_B, [&] { b2b_pencil_chunk(t - 2, ch, true, 6); });
     if (t - 4 >= 0 && t - 4 < nch) comm_op(t - 4, E_Z, E_BF, [&] { b2b_pencil_chunk(t - 4, ch, false, 3); });
     if (t - 6 >= 0 && t - 6 < nch) comm_op(t - 6, E_XF, -1, [&] { a2a_slab_chunk(t - 6, ch, false, 3); });

@@ -241,7 +241,7 @@ class Solver {
   // inside its graph) or, after anything that recomputed the outputs (prepare()), eagerly before
   // the step.  presend_done_: that exchange has been issued for the next substep 0.
   bool presend_done_ = false;
-  bool kb_overlap() const { return nkb_ > 1 && comm_ && !plan_.pencil(); }
+  bool kb_overlap() const { return nkb_ > 1 && comm_ != nullptr; }
   void presend_backward(bool wait_blocks);
   int kb_gstart(int c, int b) const;       // global retained-kx start of block b of column rank c
   int kb_gcount(int c, int b) const;
