@@ -1,3 +1,6 @@
+# Same-box A/B of the current tree against a baseline commit built in a worktree at ./ab_base
+# (git worktree add -f ab_base <commit> && (cd ab_base && python tools/build.py)); GPU tests first.
+# Used for profiles/r03s3/kspec_zero_spill.txt.  Remove the worktree afterwards (it travels with gpurun).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_solver_gpu.py tests/test_kernels_gpu.py -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/sp_tests.log 2>&1 || { tail -n 30 gpurun_out/sp_tests.log; exit 1; }
