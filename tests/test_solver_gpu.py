@@ -44,7 +44,8 @@ def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
         assert rel(gU, o.U) < 1e-11, f"U step {it}"
 
 
-@pytest.mark.parametrize("precision,NY", [("fp32", 129), ("fp64", 129), ("fp32", 257), ("fp64", 257), ("fp32", 385),
+@pytest.mark.parametrize("precision,NY", [("fp32", 129), ("fp64", 129), ("fp32", 225), ("fp64", 225), ("fp32", 257),
+                                          ("fp64", 257), ("fp32", 385),
                                           ("fp32", 633), ("fp64", 633), ("fp32", 769), ("fp32", 1201),
                                           ("fp64", 1409)])
 def test_gpu_matches_oracle_large_ny(native, precision, NY):
