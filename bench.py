@@ -107,6 +107,13 @@ def main() -> None:
     from channel_gpu_amd.parallel.native_bootstrap import init_native
     from channel_gpu_amd.utils.config import default_config
 
+    if args.gpus > 1:
+        # a first multi-GPU run must fail diagnosably, well inside the driver's time limit: the
+        # communication watchdog raises on every rank after 120 s without progress (instead of a
+        # kill with no diagnosis), and each rank prints a stderr line after the eager warm-up step,
+        # the graph capture and the first replay
+        os.environ.setdefault("CHANNEL_COMM_TIMEOUT_S", "120")
+        os.environ.setdefault("CHANNEL_MARKERS", "1")
     ri = init_native()
     rank, world = ri.rank, ri.world
     if world != args.gpus:

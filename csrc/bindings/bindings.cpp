@@ -170,6 +170,7 @@ torch::Tensor field_tensor(Solver& s, int f) {
   const Plan& p = s.plan();
   // a [y][kx][kz] view only exists for the plain layout (kx sub-blocks: use get_state)
   CH_CHECK(s.kblocks() == 1, "field(): the spectral fields are stored as " << s.kblocks() << " kx sub-blocks");
+  CH_CHECK(s.spec_kzb() == 0, "field(): the spectral fields are blocked by kz lines (use get_state)");
   auto opts = torch::TensorOptions()
                   .dtype(s.fp64() ? torch::kComplexDouble : torch::kComplexFloat)
                   .device(torch::kCUDA, c10::hip::current_device());

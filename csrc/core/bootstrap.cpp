@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
@@ -75,14 +76,15 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
     sockaddr_in sa{};
     sa.sin_family = AF_INET;
     sa.sin_port = htons(static_cast<uint16_t>(port));
-    // Listen on every interface: a MASTER_ADDR hostname may resolve to a loopback alias on the
-    // master (127.0.1.1 via /etc/hosts) or to an address that is not local (NAT), and binding to it
-    // would strand the remote peers.  The peers are checked by their announced rank below.
-    // CHANNEL_BOOTSTRAP_BIND_MASTER=1 binds to MASTER_ADDR instead (falling back to every interface
-    // when it resolves to loopback or the bind fails).
+    // Bind to MASTER_ADDR (only the interface the peers were told to use accepts connections; for
+    // 127.0.0.1 that is the local host only).  Fallback to every interface when the address is not
+    // local (NAT) so the bind fails, or when CHANNEL_BOOTSTRAP_BIND_ANY=1 (multi-node runs whose
+    // MASTER_ADDR hostname resolves to a loopback alias on the master only).  Peers identify
+    // themselves by rank; a duplicate or out-of-range rank is rejected below.
     sa.sin_addr.s_addr = htonl(INADDR_ANY);
     bool bound = false;
-    if (const char* bm = std::getenv("CHANNEL_BOOTSTRAP_BIND_MASTER"); bm && std::atoi(bm) == 1) {
+    const char* ba = std::getenv("CHANNEL_BOOTSTRAP_BIND_ANY");
+    if (!(ba && std::atoi(ba) == 1)) {
       addrinfo hints{}, *res = nullptr;
       hints.ai_family = AF_INET;
       hints.ai_socktype = SOCK_STREAM;
@@ -90,8 +92,10 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
         sockaddr_in m = sa;
         m.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
         freeaddrinfo(res);
-        const bool loop = (ntohl(m.sin_addr.s_addr) >> 24) == 127;
-        bound = !loop && ::bind(ls, reinterpret_cast<sockaddr*>(&m), sizeof(m)) == 0;
+        bound = ::bind(ls, reinterpret_cast<sockaddr*>(&m), sizeof(m)) == 0;
+        if (!bound)
+          std::fprintf(stderr, "[channel] bootstrap: cannot bind MASTER_ADDR %s; listening on every interface\n",
+                       addr.c_str());
       }
     }
     CH_CHECK(bound || ::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0,

@@ -280,6 +280,7 @@ void ShmComm::barrier() {
   } else {
     const auto t0 = std::chrono::steady_clock::now();
     while (h->sense.load() != my_sense) {
+      CH_CHECK(!failed_, "ShmComm: communicator was aborted");
       if (timeout_s_ > 0 && std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_) {
         failed_ = true;
         CH_CHECK(false, "ShmComm barrier timeout after " << timeout_s_ << " s (a peer rank died or hung)");

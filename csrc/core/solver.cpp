@@ -133,6 +133,7 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
     const char* gm = std::getenv("CHANNEL_GRAPH_MULTI");
     if (!comm_->graph_capturable() || (gm && std::atoi(gm) == 0)) use_graph_ = false;
     if (const char* t = std::getenv("CHANNEL_COMM_TIMEOUT_S")) comm_timeout_s_ = std::atof(t);
+    if (const char* m = std::getenv("CHANNEL_MARKERS")) markers_ = std::atoi(m) == 1;
     if (plan_.pencil()) {
       // one communicator per decomposition axis (collective: same call order on every rank)
       std::vector<int> col, row;
@@ -169,7 +170,13 @@ Solver::~Solver() {
 
 void Solver::alloc() {
   const Plan& p = plan_;
-  spec_ = p.spec_elems();
+  // blocked spectral layout at one rank (CHANNEL_SPEC_KZB=0: the plain [y][line] layout, A/B);
+  // P > 1 keeps [y][line]: its exchange blocks are row ranges of every line
+  kzb_ = comm_ ? 0 : kSpecKzBlock;
+  if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
+  nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
+  canon_ = p.spec_elems();
+  spec_ = static_cast<size_t>(p.NY) * p.nkx_loc * nkzs_;
   physn_ = p.phys_elems();
   // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
   // every rank (a function of Pc and the environment), at most 8 exchange segments in total
@@ -332,23 +339,27 @@ size_t Solver::kb_index(int y, int ikx, int kz) const {
   while (b > 0 && ikx < kb_start_[b]) --b;
   return kb_off_[b] + (static_cast<size_t>(y) * kb_cnt_[b] + (ikx - kb_start_[b])) * plan_.nkz_loc + kz;
 }
+size_t Solver::dev_index(int y, int ikx, int kz) const {
+  if (kzb_) return spec_index(kzb_, plan_.NY, plan_.nkx_loc, nkzs_, y, ikx, kz);
+  return kb_index(y, ikx, kz);
+}
 
 // ---- state ------------------------------------------------------------------------------------
 void Solver::set_state(const std::complex<double>* phi, const std::complex<double>* omega, const double* U) {
   const Plan& p = plan_;
   const int lines = p.lines_loc();
-  std::vector<std::complex<double>> om(omega, omega + spec_);
+  std::vector<std::complex<double>> om(omega, omega + canon_);
   if (p.owns_mean()) {
     for (int j = 0; j < p.NY; ++j) om[static_cast<size_t>(j) * lines] = std::complex<double>(U ? U[j] : 0.0, 0.0);
   }
   std::vector<std::complex<double>> phb;
-  if (nkb_ > 1) {  // [y][kx_local][kz] -> kx sub-blocks
-    phb.resize(spec_);
-    std::vector<std::complex<double>> omb(spec_);
+  if (nkb_ > 1 || kzb_) {  // [y][kx_local][kz] -> kx sub-blocks / kz line blocks (padding: 0)
+    phb.assign(spec_, 0.0);
+    std::vector<std::complex<double>> omb(spec_, 0.0);
     for (int y = 0; y < p.NY; ++y)
       for (int i = 0; i < p.nkx_loc; ++i)
         for (int k = 0; k < p.nkz_loc; ++k) {
-          const size_t src = (static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k, dst = kb_index(y, i, k);
+          const size_t src = (static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k, dst = dev_index(y, i, k);
           phb[dst] = phi[src];
           omb[dst] = om[src];
         }
@@ -376,27 +387,28 @@ void Solver::set_state(const std::complex<double>* phi, const std::complex<doubl
 void Solver::get_state(std::complex<double>* phi, std::complex<double>* omega, double* U) const {
   const Plan& p = plan_;
   HIP_CHECK(hipStreamSynchronize(s_comp_));
+  // device layout -> canonical [y][kx_local][kz]
   auto fetch = [&](int f, std::complex<double>* dst) {
+    std::vector<std::complex<double>> t(spec_);
     if (fp64_) {
       std::vector<double2> h(spec_);
       HIP_CHECK(hipMemcpy(h.data(), field_ptr(f), spec_ * esz_, hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < spec_; ++i) dst[i] = {h[i].x, h[i].y};
+      for (size_t i = 0; i < spec_; ++i) t[i] = {h[i].x, h[i].y};
     } else {
       std::vector<float2> h(spec_);
       HIP_CHECK(hipMemcpy(h.data(), field_ptr(f), spec_ * esz_, hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < spec_; ++i) dst[i] = {h[i].x, h[i].y};
+      for (size_t i = 0; i < spec_; ++i) t[i] = {h[i].x, h[i].y};
     }
+    if (nkb_ == 1 && !kzb_) {
+      std::copy(t.begin(), t.end(), dst);
+      return;
+    }
+    for (int y = 0; y < p.NY; ++y)
+      for (int i = 0; i < p.nkx_loc; ++i)
+        for (int k = 0; k < p.nkz_loc; ++k) dst[(static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k] = t[dev_index(y, i, k)];
   };
   fetch(PHI, phi);
   fetch(OMEGA, omega);
-  if (nkb_ > 1) {  // kx sub-blocks -> [y][kx_local][kz]
-    for (auto* q : {phi, omega}) {
-      std::vector<std::complex<double>> t(q, q + spec_);
-      for (int y = 0; y < p.NY; ++y)
-        for (int i = 0; i < p.nkx_loc; ++i)
-          for (int k = 0; k < p.nkz_loc; ++k) q[(static_cast<size_t>(y) * p.nkx_loc + i) * p.nkz_loc + k] = t[kb_index(y, i, k)];
-    }
-  }
   const int lines = p.lines_loc();
   for (int j = 0; j < p.NY; ++j) {
     if (p.owns_mean()) {
@@ -411,7 +423,7 @@ void Solver::get_state(std::complex<double>* phi, std::complex<double>* omega, d
 void Solver::init_ic() {
   const Plan& p = plan_;
   const int N = p.NY, lines = p.lines_loc();
-  std::vector<std::complex<double>> phi(spec_), om(spec_);
+  std::vector<std::complex<double>> phi(canon_), om(canon_);
   std::vector<double> U(N);
   const auto& y = grid_.y;
   for (int j = 0; j < N; ++j) U[j] = (cfg_.ic == "zero") ? 0.0 : 0.75 * cfg_.Q * (1.0 - y[j] * y[j]);
@@ -506,8 +518,9 @@ void Solver::kspec(int mode, int n, bool stats) {
   const Plan& p = plan_;
   SpecArgs a;
   a.N = p.NY;
-  a.lines = p.lines_loc();
-  a.nkz = p.nkz_loc;
+  a.lines = p.nkx_loc * nkzs_;
+  a.nkz = nkzs_;
+  a.kzb = kzb_;
   a.kz0 = p.kz0;
   a.kx0 = p.kx0;
   a.nkx = p.nkx;
@@ -552,7 +565,7 @@ void Solver::kspec(int mode, int n, bool stats) {
       SpecArgs ab = a;
       const size_t off = kb_off_[b] * esz_;
       auto sh = [&](void* q) { return static_cast<void*>(static_cast<char*>(q) + off); };
-      ab.lines = kb_cnt_[b] * p.nkz_loc;
+      ab.lines = kb_cnt_[b] * nkzs_;
       ab.kx0 = p.kx0 + kb_start_[b];
       ab.phi = sh(a.phi);
       ab.omega = sh(a.omega);
@@ -735,6 +748,12 @@ void Solver::transforms(int n, bool /*stats*/) {
   da.dy_uniform = 2.0 / (p.NY - 1);
 
   if (!comm_) {
+    // one rank: the spectral fields are blocked by 8 kz lines (kzb_, spec_index); the x transforms
+    // address rows spec_y0 .. of the full fields
+    xa.kzb = kzb_;
+    xa.nkzs = nkzs_;
+    xa.spec_ny = p.NY;
+    xa.spec_y0 = 0;
     XSrc src;
     src.base = out_;
     src.nsrc = 1;
@@ -767,10 +786,11 @@ void Solver::transforms(int n, bool /*stats*/) {
       for (int y0 = 0; y0 < p.ny_loc; y0 += ychunk_, ++ci) {
         const int ny = std::min(ychunk_, p.ny_loc - y0);
         hipStream_t cs = streams[ci % nst];
-        const size_t so = static_cast<size_t>(y0) * p.nkx * p.nkz * esz_;
+        const size_t so = kzb_ ? 0 : static_cast<size_t>(y0) * p.nkx * p.nkz * esz_;
         char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz * esz_;
         XArgs xc = xa;
         xc.ny = ny;
+        if (kzb_) xc.spec_y0 = y0;
         XSrc sc = src;
         sc.base = static_cast<char*>(out_) + so;
         xc.nfields = 6;
@@ -1319,6 +1339,7 @@ void Solver::step_body(bool stats) {
   for (int n = 0; n < 3; ++n) {
     transforms(n, false);
     kspec(1, n, stats && n == 2);
+    CH_CHECK(!capture_fail_test_, "capture failure injected (CHANNEL_TEST_CAPTURE_FAIL)");
   }
   // the next step's substep-0 backward exchange of blocks 0 .. NB-2, behind this step's last
   // K-SPEC blocks (joined back into the compute stream: a captured graph must end there)
@@ -1345,10 +1366,38 @@ void Solver::presend_backward(bool wait_blocks) {
   presend_done_ = true;
 }
 
+void Solver::marker(const char* what) {
+  const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_created_).count();
+  std::fprintf(stderr, "[channel] rank %d/%d: %s (step %ld, %.2f s after setup)\n", plan_.rank, plan_.P, what, nstep_, t);
+  std::fflush(stderr);
+}
+
+// A capture that threw: end it on the origin stream and make sure no stream forked into it is
+// left in capture mode (a later collective on such a stream would fail on this rank only and strand
+// its peers in the capture agreement below).
+void Solver::end_failed_capture() {
+  hipGraph_t junk = nullptr;
+  (void)hipStreamEndCapture(s_comp_, &junk);
+  if (junk) (void)hipGraphDestroy(junk);
+  std::vector<hipStream_t> forked = {s_comm_};
+  for (auto st : s_extra_) forked.push_back(st);
+  for (auto st : forked) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+      hipGraph_t j2 = nullptr;
+      (void)hipStreamEndCapture(st, &j2);
+      if (j2) (void)hipGraphDestroy(j2);
+    }
+  }
+  (void)hipGetLastError();
+}
+
 void Solver::step(bool stats_for_next) {
   if (!prepared_) prepare();
   const int gi = stats_for_next ? 1 : 0;
   bool done = false;
+  const bool warmup_step = comm_ && !comm_warm_;
+  bool captured_now = false;
   if (step_timing_) {
     if (step_ev_used_ == step_ev_.size()) {
       hipEvent_t a, b;
@@ -1373,13 +1422,18 @@ void Solver::step(bool stats_for_next) {
           mode = ms == "global" ? hipStreamCaptureModeGlobal
                                 : (ms == "relaxed" ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal);
         }
+        // test-only (CHANNEL_TEST_CAPTURE_FAIL=<rank>): that rank's capture fails after the first
+        // substep has been recorded, to drive the cross-rank agreement below
+        const char* tf = std::getenv("CHANNEL_TEST_CAPTURE_FAIL");
+        const bool inject = tf && std::atoi(tf) == plan_.rank;
         HIP_CHECK(hipStreamBeginCapture(s_comp_, mode));
         try {
+          capture_fail_test_ = inject;
           step_body(stats_for_next);
+          capture_fail_test_ = false;
         } catch (...) {
-          hipGraph_t junk = nullptr;
-          (void)hipStreamEndCapture(s_comp_, &junk);
-          if (junk) (void)hipGraphDestroy(junk);
+          capture_fail_test_ = false;
+          end_failed_capture();
           throw;
         }
         HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
@@ -1392,17 +1446,25 @@ void Solver::step(bool stats_for_next) {
         use_graph_ = false;
       }
       graph_ok_[gi] = true;
-      if (comm_ && plan_.P > 1) {
+      captured_now = true;
+      if (comm_) {
         // every rank must replay the same exchange sequence: if capture failed anywhere, all ranks
         // drop their graphs and step eagerly (no rank may launch a captured RCCL sequence that a
-        // peer runs eagerly in a different order)
+        // peer runs eagerly in a different order).  An error here aborts every communicator, so
+        // the peers waiting in this allreduce fail too instead of hanging.
         unsigned* flag = d_health_ + 1;
         const unsigned mine = gexec_[gi] ? 0u : 1u;
-        HIP_CHECK(hipMemcpyAsync(flag, &mine, sizeof(unsigned), hipMemcpyHostToDevice, s_comm_));
-        comm_->allreduce_max_u32(flag, 1, s_comm_);
         unsigned any = 0;
-        HIP_CHECK(hipMemcpyAsync(&any, flag, sizeof(unsigned), hipMemcpyDeviceToHost, s_comm_));
-        wait(s_comm_);
+        try {
+          HIP_CHECK(hipMemcpyAsync(flag, &mine, sizeof(unsigned), hipMemcpyHostToDevice, s_comm_));
+          comm_->allreduce_max_u32(flag, 1, s_comm_);
+          HIP_CHECK(hipMemcpyAsync(&any, flag, sizeof(unsigned), hipMemcpyDeviceToHost, s_comm_));
+          wait(s_comm_);
+        } catch (...) {
+          abort_comms();
+          throw;
+        }
+        HIP_CHECK(hipMemsetAsync(flag, 0, sizeof(unsigned), s_comm_));
         if (any) {
           if (gexec_[gi]) {
             (void)hipGraphExecDestroy(gexec_[gi]);
@@ -1420,6 +1482,18 @@ void Solver::step(bool stats_for_next) {
   }
   if (!done) step_body(stats_for_next);
   comm_warm_ = true;
+  if (markers_) {
+    if (warmup_step) {
+      synchronize();
+      marker("eager warm-up step done (RCCL peers connected)");
+    }
+    if (captured_now) marker(gexec_[gi] ? "step graph captured" : "step graph not captured: stepping eagerly");
+    if (done && !replayed_[gi]) {
+      synchronize();
+      replayed_[gi] = true;
+      marker(gi ? "first replay of the statistics step graph done" : "first replay of the step graph done");
+    }
+  }
   if (step_timing_) HIP_CHECK(hipEventRecord(step_ev_[step_ev_used_++].second, s_comp_));
   if (phase_timing_) flush_phase_events();
   if (stats_for_next) stats_pending_ = true;
@@ -1448,16 +1522,22 @@ void Solver::wait(hipStream_t s) {
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) HIP_CHECK(e);
     if (comm_failed()) {
-      comm_->abort();
+      abort_comms();
       CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
     }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (comm_timeout_s_ > 0 && el > comm_timeout_s_) {
-      comm_->abort();
+      abort_comms();
       CH_CHECK(false, "rank " << plan_.rank << ": no progress for " << comm_timeout_s_ << " s; communicator aborted");
     }
     if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
+}
+
+void Solver::abort_comms() {
+  if (comm_row_) comm_row_->abort();
+  if (comm_col_) comm_col_->abort();
+  if (comm_) comm_->abort();
 }
 
 bool Solver::comm_failed() {
@@ -1475,12 +1555,12 @@ void Solver::wait_event(hipEvent_t e) {
     if (r == hipSuccess) return;
     if (r != hipErrorNotReady) HIP_CHECK(r);
     if (comm_failed()) {
-      comm_->abort();
+      abort_comms();
       CH_CHECK(false, "communicator failure on rank " << plan_.rank << " (peer died or network error)");
     }
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (comm_timeout_s_ > 0 && el > comm_timeout_s_) {
-      comm_->abort();
+      abort_comms();
       CH_CHECK(false, "rank " << plan_.rank << ": no progress for " << comm_timeout_s_ << " s; communicator aborted");
     }
     if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
@@ -1569,8 +1649,8 @@ std::vector<double> Solver::mean_profile() {
 void Solver::symmetrize() {
   const Plan& p = plan_;
   if (!comm_) {
-    symmetrize_kz0(field_ptr(PHI), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
-    symmetrize_kz0(field_ptr(OMEGA), p.NY, p.nkx, p.nkz, p.Kx, fp64_, s_comp_);
+    symmetrize_kz0(field_ptr(PHI), p.NY, p.nkx, nkzs_, p.Kx, kzb_, fp64_, s_comp_);
+    symmetrize_kz0(field_ptr(OMEGA), p.NY, p.nkx, nkzs_, p.Kx, kzb_, fp64_, s_comp_);
     prepared_ = false;
     return;
   }
@@ -1734,7 +1814,7 @@ void Solver::run(long nsteps, bool verbose) {
         }
         std::fprintf(stderr, "[channel] non-finite state detected at step %ld (t=%g, dt=%g); aborting\n", L.step,
                      L.time, L.dt);
-        if (comm_) comm_->abort();
+        if (comm_) abort_comms();
         CH_CHECK(false, "health check failed at step " << L.step);
       }
       if (rb && nstep_ - snap_step_ >= sn) take_snapshot();
@@ -1782,7 +1862,12 @@ bool Solver::t_end_reached() {
   if (have_prev) {
     wait_event(ev_tdt_[cur ^ 1]);
     const double dt = h_tdt_[2 * (cur ^ 1)], t = h_tdt_[2 * (cur ^ 1) + 1];  // d_dt_, d_time_ adjacent
-    if (t + 3.0 * dt < cfg_.t_end) return false;
+    // the step just queued advances the time by at most dt_max (dt_fixed when set): only within
+    // that margin of t_end is the device time read synchronously (dt can jump to dt_max at once,
+    // e.g. from a zero-velocity state, so a multiple of the previous dt is no bound)
+    const double margin = cfg_.dt_fixed > 0.0 ? cfg_.dt_fixed : cfg_.dt_max;
+    if (margin > 0.0 && t + (1.0 + 1e-12) * margin < cfg_.t_end) return false;
+    (void)dt;
   }
   return time() >= cfg_.t_end;
 }
@@ -1831,7 +1916,7 @@ void Solver::rollback() {
 void Solver::inject_nan(int f) {
   presend_done_ = false;
   // an interior point of line 1 of the field (line 0 on the owner rank holds U)
-  const size_t elem = kb_index(plan_.NY / 2, 0, 0) + std::min(1, plan_.lines_loc() - 1);
+  const size_t elem = plan_.nkz_loc > 1 ? dev_index(plan_.NY / 2, 0, 1) : dev_index(plan_.NY / 2, std::min(1, plan_.nkx_loc - 1), 0);
   ::channel::inject_nan(field_ptr(f), elem, fp64_, s_comp_);
   HIP_CHECK(hipStreamSynchronize(s_comp_));
 }
@@ -1859,10 +1944,13 @@ Solver::Spectra Solver::spectra() {
   a.u = field_ptr(OUT0);
   a.v = field_ptr(OUT1);
   a.w = field_ptr(OUT2);
-  a.lines = p.lines_loc();
+  a.lines = p.nkx_loc * nkzs_;
   a.nkx_loc = p.nkx_loc;
   a.kx0 = p.kx0;
   a.nkz_loc = p.nkz_loc;
+  a.nkzs = nkzs_;
+  a.kzb = kzb_;
+  a.N = p.NY;
   a.kz0 = p.kz0;
   a.nkx = p.nkx;
   a.Kx = p.Kx;
@@ -1878,7 +1966,7 @@ Solver::Spectra Solver::spectra() {
     ab.u = static_cast<const char*>(a.u) + off;
     ab.v = static_cast<const char*>(a.v) + off;
     ab.w = static_cast<const char*>(a.w) + off;
-    ab.lines = kb_cnt_[b] * p.nkz_loc;
+    ab.lines = kb_cnt_[b] * nkzs_;
     ab.nkx_loc = kb_cnt_[b];
     ab.kx0 = p.kx0 + kb_start_[b];
     spectra_accumulate(ab, fp64_, s_comp_);
@@ -1969,8 +2057,8 @@ Solver::RestartJob Solver::capture_restart(const std::string& g, const std::stri
   j.g = g;
   j.ddv = ddv;
   j.umean = umean;
-  j.phi.resize(spec_);
-  j.om.resize(spec_);
+  j.phi.resize(canon_);
+  j.om.resize(canon_);
   j.U.resize(plan_.NY);
   get_state(j.phi.data(), j.om.data(), j.U.data());
   double hv[2];
@@ -2116,7 +2204,7 @@ void Solver::read_restart(const std::string& g, const std::string& ddv, const st
   const double N2 = static_cast<double>(p.NX) * p.Nzp;
   std::vector<int> planes(p.nkx_loc);
   for (int i = 0; i < p.nkx_loc; ++i) planes[i] = p.kx_fft_pos(p.kx0 + i);
-  std::vector<std::complex<double>> phi(spec_, 0.0), om(spec_, 0.0);
+  std::vector<std::complex<double>> phi(canon_, 0.0), om(canon_, 0.0);
   auto unpack = [&](const std::string& path, std::vector<std::complex<double>>& f) {
     std::vector<double> d;
     int dims[3];

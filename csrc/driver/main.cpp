@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
     solver.reset();
   } catch (const std::exception& e) {
     std::fprintf(stderr, "[rank %d] fatal: %s\n", pi.rank, e.what());
-    if (solver && solver->comm()) solver->comm()->abort();  // do not leave peers hanging
+    if (solver) solver->abort_comms();  // do not leave peers hanging
     std::fflush(stderr);
     std::_Exit(1);
   }

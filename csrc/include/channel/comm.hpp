@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <memory>
 #include <string>
@@ -109,7 +110,7 @@ class ShmComm final : public Comm {
 
  private:
   void barrier();
-  bool failed_ = false;
+  std::atomic<bool> failed_{false};  // set by abort() (any thread): the barrier then raises at once
   double timeout_s_ = 300.0;  // CHANNEL_COMM_TIMEOUT_S
   char* slot(int src, int dst);
   template <typename T, typename Op>

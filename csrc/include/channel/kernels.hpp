@@ -47,12 +47,29 @@ struct DenseD1Dev {
 };
 void d1_dense_mfma(const DenseD1Dev& m, const void* in, void* out, int lines, hipStream_t stream);
 
+// ---- spectral field layout ----------------------------------------------------------------------
+// Element (y, local kx ikx, local kz) of a spectral field of nkx local kx and kz line stride nkzs
+// (a K-SPEC line is ikx * nkzs + kz).  kzb = 0: [y][kx][kz], every y plane contiguous (the exchange
+// blocks of P > 1 are row ranges).  kzb = 8 (one rank): [kz / 8][kx][y][kz % 8] with nkzs a
+// multiple of 8, so a block of 8 kz lines is one contiguous NY x 8 region: K-SPEC's tiles (4 lines
+// x all y) then read and write contiguous memory instead of 32-byte pieces one plane (~1.9 MB at
+// the headline grid) apart (tools/tilebench.hip: 2.5 -> 4.2 TB/s for that access pattern at
+// K-SPEC's occupancy); the x transforms still move 64-byte pieces (8 kz columns of one plane),
+// and the kx rows of one kz block stay within NX/1.5 * NY * 64 B (kz-block-major: a kx-major
+// block order spread one x-transform tile over the whole field).
+constexpr int kSpecKzBlock = 8;
+__host__ __device__ inline size_t spec_index(int kzb, int N, int nkx, int nkzs, int y, int ikx, int kz) {
+  return kzb ? (((static_cast<size_t>(kz / kSpecKzBlock) * nkx + ikx) * N + y) * kSpecKzBlock + kz % kSpecKzBlock)
+             : (static_cast<size_t>(y) * nkx + ikx) * nkzs + kz;
+}
+
 // ---- the fused spectral (y-line) substep kernel ---------------------------------------------
 struct SpecArgs {
   // geometry
   int N = 0;              // NY
   int lines = 0;          // local lines = nkx_loc * nkz, line = ikx_local * nkz + kz
-  int nkz = 0, kx0 = 0, nkx = 0, Kx = 0;   // nkz = local kz count (pencil: a kz range)
+  int nkz = 0, kx0 = 0, nkx = 0, Kx = 0;   // nkz = local kz line stride (pencil: a kz range; kzb: padded to 8)
+  int kzb = 0;            // spectral layout (spec_index)
   int kz0 = 0;            // first local kz (pencil)
   double ax = 1, az = 2;  // 2 pi / LX, 2 pi / LZ
   double nu = 1.0 / 3250.0;
@@ -140,6 +157,9 @@ struct XArgs {
   int zero_mean_field = -1;
   int kz_glob0 = 0;
   int lds_poison = 0;                // debug: fill the LDS with NaN before use
+  // blocked spectral layout (one rank, one source block; spec_index with kzb = 8): rows spec_y0 ..
+  // spec_y0 + ny - 1 of fields of spec_ny rows and line stride nkzs
+  int kzb = 0, nkzs = 0, spec_ny = 0, spec_y0 = 0;
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
@@ -182,7 +202,7 @@ struct DtArgs {
 void dt_update(const DtArgs& a, hipStream_t s);
 
 // kz=0 plane Hermitian symmetrisation of a [y][nkx][nkz] field held entirely by one rank
-void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStream_t s);
+void symmetrize_kz0(void* q, int N, int nkx, int nkzs, int Kx, int kzb, bool fp64, hipStream_t s);
 // distributed version: pack the local kz=0 column [y][kx_loc], exchange, symmetrise from the
 // gathered columns (blocks [c][y][nkx_c] of the ranks of this process row)
 struct Kz0SymArgs {
@@ -197,6 +217,7 @@ void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool
 struct SpectraArgs {
   const void *u = nullptr, *v = nullptr, *w = nullptr;  // spectral [NY][lines], lines = nkx_loc*nkz_loc
   int lines = 0, nkx_loc = 0, kx0 = 0, nkz_loc = 0, kz0 = 0;
+  int nkzs = 0, kzb = 0, N = 0;       // line stride in kz, layout (spec_index), NY
   int nkx = 0, Kx = 0, nkz = 0;       // global retained counts
   const int* planes = nullptr;        // device [nplanes] y indices
   int nplanes = 0;

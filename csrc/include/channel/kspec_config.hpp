@@ -23,6 +23,9 @@ struct Cplx<double> {
 // lines make 2 waves per SIMD.
 template <int R, typename T>
 constexpr int kspec_lines() {
+#ifdef CH_KSPEC_W7
+  if (R == 7) return CH_KSPEC_W7;
+#endif
   return R <= 4 ? 8 : 4;
 }
 

@@ -18,6 +18,7 @@
 #include <functional>
 #include <memory>
 #include <thread>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -130,6 +131,10 @@ class Solver {
   const YTablesDev& ytables() const { return ytab_; }
   // kx sub-blocks of the local spectral layout (1 = plain [y][kx_local][kz]; see nkb_)
   int kblocks() const { return nkb_; }
+  int spec_kzb() const { return kzb_; }  // spectral layout (spec_index)
+  // abort every communicator (the per-axis split ones first: aborting the parent does not abort
+  // communicators split from it), so no stream stays blocked in an exchange with a dead peer
+  void abort_comms();
   void substep_debug(int n);            // one substep, eager (tests)
   void transforms_debug(bool dt_update);  // backward + phys + forward only (tests)
   Comm* comm() { return comm_.get(); }
@@ -199,6 +204,11 @@ class Solver {
   void* xbuf_ = nullptr;   // P>1: 6 * ny_loc*nkx*nkz_loc (A-exchange blocks)
   void* zbuf_ = nullptr;   // pencil: 6 * ny_loc*nx_loc*nkz (B-exchange blocks, z stage in place)
   size_t spec_ = 0, physn_ = 0, xstride_ = 0, zstride_ = 0;
+  // spectral layout (spec_index): kzb_ = 8 (one rank) blocks the lines by 8 kz, with the kz line
+  // stride nkzs_ padded to a multiple of 8; canon_ = NY * nkx_loc * nkz_loc, the element count of
+  // the canonical host layout [y][kx_loc][kz_loc] (set_state / get_state / restart files)
+  int kzb_ = 0, nkzs_ = 0;
+  size_t canon_ = 0;
 
   // device scalars / diagnostics (one allocation)
   void* dscal_ = nullptr;
@@ -246,6 +256,7 @@ class Solver {
   int kb_gstart(int c, int b) const;       // global retained-kx start of block b of column rank c
   int kb_gcount(int c, int b) const;
   size_t kb_index(int y, int ikx, int kz) const;  // blocked element index of (y, local kx, kz)
+  size_t dev_index(int y, int ikx, int kz) const;  // device element index of (y, local kx, local kz)
   // phase timing: event pool and the (phase, start, end) pairs of the current step
   struct TPair {
     int phase;
@@ -284,6 +295,15 @@ class Solver {
 
   bool use_graph_ = true;
   bool graph_ok_[2] = {false, false};
+  // CHANNEL_MARKERS=1 (bench.py sets it at P > 1): one stderr line per rank after the eager warm-up
+  // step, the capture and the first replay of each step graph, each after a (watchdog-polled)
+  // synchronisation, so a first multi-GPU run that hangs shows which stage and rank stopped
+  bool markers_ = false;
+  bool capture_fail_test_ = false;
+  bool replayed_[2] = {false, false};
+  std::chrono::steady_clock::time_point t_created_ = std::chrono::steady_clock::now();
+  void marker(const char* what);
+  void end_failed_capture();
   hipGraphExec_t gexec_[2] = {nullptr, nullptr};
   bool prepared_ = false;
   long nstep_ = 0;

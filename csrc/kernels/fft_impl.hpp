@@ -120,6 +120,14 @@ inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
   return m >= NT / C ? kSegWin : kSegFull;
 }
 
+// element offset of (row y of the chunk, retained kx i, kz) in a blocked spectral field (spec_index
+// with kzb = 8; XArgs::spec_y0 / spec_ny / nkzs)
+__device__ __forceinline__ unsigned spec_blk_off(const XArgs& a, int y, int i, int kz) {
+  const unsigned blk = static_cast<unsigned>((kz / kSpecKzBlock) * a.nkx + i);
+  return (blk * static_cast<unsigned>(a.spec_ny) + static_cast<unsigned>(a.spec_y0 + y)) * kSpecKzBlock +
+         static_cast<unsigned>(kz % kSpecKzBlock);
+}
+
 // V consecutive complex values moved by one global access (V = 2 for fp32: 16-byte loads and
 // stores, half the instructions of 8-byte ones; the stores of the x kernels were issue-bound)
 template <typename T2, int V>
@@ -134,7 +142,9 @@ struct alignas(sizeof(T2) * V) CVec {
 // block's lifetime (SQ_WAIT_ANY ~73 % of wave cycles at ~2 TB/s).  Twiddles are staged once.
 // SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
 // compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
-template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1>
+// SL = 1: blocked spectral layout (XArgs::kzb, one rank: SM = kSegOne); tiles then walk y fastest,
+// so the tiles of one XCD share the 128-byte lines two planes of a kz block fill
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -160,10 +170,24 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int tid = threadIdx.x;
   const int nload = a.nkx * CW;
   CV v[EPT];
+  static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
   // tile t -> (f, y, kz0); at each iteration the blocks of one XCD take consecutive tiles
+  auto decode = [&](int t, int& f, int& y, int& kz0) {
+    if constexpr (SL) {
+      y = t % a.ny;
+      const int rest = t / a.ny;
+      kz0 = (rest % nkzc) * C;
+      f = rest / nkzc;
+    } else {
+      kz0 = (t % nkzc) * C;
+      const int rest = t / nkzc;
+      y = rest % a.ny;
+      f = rest / a.ny;
+    }
+  };
   auto fetch = [&](int t) {
-    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
-    const int y = rest % a.ny, f = rest / a.ny;
+    int f, y, kz0;
+    decode(t, f, y, kz0);
     const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
     // this rank's own block is read in place from its spectral field (no self exchange)
     const T2* sbase = src.self_seg >= 0 ? static_cast<const T2*>(src.self_base) + f * src.self_field_stride : base;
@@ -174,7 +198,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       // columns kz >= nkz are transformed (independently) but never stored
       const int i = min(e / CW, a.nkx - 1);
       const int kz = min(kz0 + (e % CW) * V, a.nkz - V);
-      if constexpr (SM == kSegOne) {
+      if constexpr (SL) {
+        v[q] = *reinterpret_cast<const CV*>(base + spec_blk_off(a, y, i, kz));
+      } else if constexpr (SM == kSegOne) {
         v[q] = *reinterpret_cast<const CV*>(
             base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
       } else {
@@ -190,8 +216,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
   for (; t < ntiles; t += G) {
-    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
-    const int y = rest % a.ny, f = rest / a.ny;
+    int f, y, kz0;
+    decode(t, f, y, kz0);
     lds_barrier();  // previous tile's stores have finished reading s
     // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
     // state, whose mean line holds U(y)); it is e = 0: thread 0, q = 0, u = 0
@@ -254,7 +280,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   }
 }
 
-template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1>
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_forward_kernel(XArgs a, const typename C2<T>::type* phys, XDst dst, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
@@ -277,9 +303,23 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
   CV v[EPT];
+  static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one destination block");
+  auto decode = [&](int t, int& f, int& y, int& kz0) {
+    if constexpr (SL) {
+      y = t % a.ny;
+      const int rest = t / a.ny;
+      kz0 = (rest % nkzc) * C;
+      f = rest / nkzc;
+    } else {
+      kz0 = (t % nkzc) * C;
+      const int rest = t / nkzc;
+      y = rest % a.ny;
+      f = rest / a.ny;
+    }
+  };
   auto fetch = [&](int t) {
-    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
-    const int y = rest % a.ny, f = rest / a.ny;
+    int f, y, kz0;
+    decode(t, f, y, kz0);
     const T2* in = phys + f * a.field_stride_phys;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
@@ -300,8 +340,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
   for (; t < ntiles; t += G) {
-    const int kz0 = (t % nkzc) * C, rest = t / nkzc;
-    const int y = rest % a.ny, f = rest / a.ny;
+    int f, y, kz0;
+    decode(t, f, y, kz0);
     lds_barrier();
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
@@ -338,7 +378,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-        if constexpr (SM == kSegOne) {
+        if constexpr (SL) {
+          *reinterpret_cast<CV*>(outb + spec_blk_off(a, y, i, kz)) = w;
+        } else if constexpr (SM == kSegOne) {
           *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
                                  static_cast<unsigned>(kz)) = w;
         } else {
@@ -391,7 +433,10 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
   // its windows, computed up front, spilled ~640 SGPRs)
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
-  auto kern = a.npseg > 1     ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
+  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
+           "xfft_backward: the blocked spectral layout needs one source block");
+  auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 1>
+              : a.npseg > 1   ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
                               : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
@@ -407,7 +452,10 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
     if (xvec_ok(a, dst.off, dst.ndst, dst.self_field_stride, 0)) return xf_launch_cfg<NN, T, WIDE, 2>(a, phys, dst, tw, s);
   }
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
-  auto kern = a.npseg > 1             ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
+  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
+           "xfft_forward: the blocked spectral layout needs one destination block");
+  auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, 1>
+              : a.npseg > 1           ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
               : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
                               : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;

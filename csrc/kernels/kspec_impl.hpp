@@ -86,6 +86,9 @@ struct Stage {
   T2* tile;   // buffer of the last staging (column() reads it)
   T2* tile2;  // the other buffer (nullptr: single-buffered)
   int N, lines, line0, w, lane;
+  // spectral layout (spec_index): element (y, line) at lineoff(line) + y * rs
+  int kzb = 0, nkzs = 1, nkx = 1;
+  unsigned rs = 0;
   // Per-thread element offset of (row y0 = tid / W, line line0 + tid % W) and of one 64-row pass:
   // re-derived per tile through an opaque copy, so the per-field addresses are formed at their
   // use (a 64-bit field base + a 32-bit offset: global_load/store saddr forms) instead of being
@@ -96,9 +99,22 @@ struct Stage {
   unsigned doff[kRegSlots || GL ? 1 : NS];
 
   static __device__ __forceinline__ int row_off(int y) { return y * PITCH + (G ? (y / R) : 0); }
+  __device__ __forceinline__ void set_layout(int kzb_, int nkzs_) {
+    kzb = kzb_;
+    nkzs = nkzs_;
+    nkx = lines / nkzs_;
+    rs = kzb ? static_cast<unsigned>(kSpecKzBlock) : static_cast<unsigned>(lines);
+  }
+  __device__ __forceinline__ unsigned lineoff(int line) const {
+    if (!kzb) return static_cast<unsigned>(line);
+    const int ikx = line / nkzs, kz = line - ikx * nkzs;
+    return (static_cast<unsigned>(kz / kSpecKzBlock) * static_cast<unsigned>(nkx) + static_cast<unsigned>(ikx)) *
+               static_cast<unsigned>(N * kSpecKzBlock) +
+           static_cast<unsigned>(kz % kSpecKzBlock);
+  }
   __device__ __forceinline__ unsigned thread_off(int l0) const {
     const int y0 = threadIdx.x / W, l = threadIdx.x % W;
-    unsigned o = static_cast<unsigned>(y0) * static_cast<unsigned>(lines) + static_cast<unsigned>(min(l0 + l, lines - 1));
+    unsigned o = static_cast<unsigned>(y0) * rs + lineoff(min(l0 + l, lines - 1));
     asm volatile("" : "+v"(o));
     return o;
   }
@@ -129,8 +145,8 @@ struct Stage {
       constexpr int RPI = 64 / DPR;  // rows per instruction
       const int lane = __lane_id();
       const int ry = lane / DPR, dw = lane % DPR;
-      const unsigned stride = static_cast<unsigned>(lines) * DPE;  // dwords per global row
-      const unsigned base = static_cast<unsigned>(min(l0 + dw / DPE, lines - 1)) * DPE + dw % DPE;
+      const unsigned stride = rs * DPE;  // dwords per global row
+      const unsigned base = lineoff(min(l0 + dw / DPE, lines - 1)) * DPE + dw % DPE;
       const unsigned* srcd = reinterpret_cast<const unsigned*>(src);
       unsigned* dstd = reinterpret_cast<unsigned*>(tile2);
       const int ninst = (N + RPI - 1) / RPI;
@@ -147,11 +163,10 @@ struct Stage {
     } else {
       const int y0 = threadIdx.x / W, l = threadIdx.x % W;
       // rows >= N read row N-1 of the same (clamped) line
-      const unsigned last = static_cast<unsigned>(N - 1) * static_cast<unsigned>(lines) +
-                            static_cast<unsigned>(min(l0 + l, lines - 1));
+      const unsigned last = static_cast<unsigned>(N - 1) * rs + lineoff(min(l0 + l, lines - 1));
 #pragma unroll
       for (int q = 0; q < R; ++q) {
-        const unsigned oq = y0 + RPB * q < N ? o + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines) : last;
+        const unsigned oq = y0 + RPB * q < N ? o + static_cast<unsigned>(RPB * q) * rs : last;
         pend[S][q] = src[oq];
       }
     }
@@ -183,7 +198,7 @@ struct Stage {
         if constexpr (kRegSlots) {
           tile[row_off(y) + l] = pend[S][q];
         } else {
-          tile[row_off(y) + l] = dsrc[S][doff[S] + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines)];
+          tile[row_off(y) + l] = dsrc[S][doff[S] + static_cast<unsigned>(RPB * q) * rs];
         }
       }
     }
@@ -223,7 +238,7 @@ struct Stage {
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         const int y = y0 + RPB * q;
-        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * static_cast<unsigned>(lines)] = tile[row_off(y) + l];
+        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * rs] = tile[row_off(y) + l];
       }
     }
   }
@@ -281,7 +296,9 @@ constexpr int kParDD = 1, kParAnalytic = 2;
 // in place of the register slots (one field ahead instead of NS)
 // (A/B record, not kept: direct register->global stores instead of the tile transposes, 9 % slower
 // at R = 7, profiles/r03s3/ab_kspec_ns7.txt)
-template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0>
+// SPLIT: 0 = the whole substep in this kernel; 1 = stop after the phi / v stores (the D1 of v and
+// omega, the statistics and the u, w, omega_x, omega_z outputs run in kspec_out_kernel)
+template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0, int SPLIT = 0>
 __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
   constexpr bool kGldsTile = (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
@@ -368,6 +385,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
+  st.set_layout(a.kzb, a.nkz);
   T2* phi = static_cast<T2*>(a.phi);
   T2* omega = static_cast<T2*>(a.omega);
   T2* Rphi = static_cast<T2*>(a.Rphi);
@@ -745,6 +763,21 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       if (__any(bad) && lane == 0) atomicOr(a.health, 1u);
     }
 
+    if constexpr (SPLIT == 1) {
+      // the output stage reads v from out[1], omega and phi from the state
+      st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);
+      if (a.mean_diag && is_mean && lane == 0) {
+        a.mean_diag[3 * N + 2] = mean_diag_flux;
+        a.mean_diag[3 * N + 3] = mean_C;
+      }
+      KSPEC_STAMP(9)
+      if (kGldsTile && has_next) {
+        ahead(std::integral_constant<int, 0>{}, next_line0);
+        if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
+        if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
+      }
+      continue;
+    }
     // ---------------- prepare velocity / vorticity for the physical-space stage --------------
     fresh();
     double dvo[4][R];  // D1 v (0, 1), D1 omega (2, 3): one 4-RHS solve
@@ -849,6 +882,215 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #undef KSPEC_STAMP
 }
 
+// K-SPEC output stage (split mode, after kspec_kernel<..., SPLIT = 1>): per line, v (out[1]),
+// omega and phi in, D1 of v and omega (one 4-RHS solve on the constant factorisation), the plane
+// statistics and the u, w, omega_x, omega_z outputs (nonLinear_kernels.cu:8-92,
+// convolution_kernels.cu:7-66, statistics.cu:7-95).  Without the advance's registers (the
+// k-dependent factorisations, the 6-RHS implicit solve) a line fits in <= 256 VGPRs at R <= 8, so
+// W = 8 lines per workgroup run two waves per SIMD: the output half of the substep was the
+// latency-bound half at one wave per SIMD (it reads 3 fields more than the fused kernel).
+template <int R, typename T, int W, int XM>
+__global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) {
+  using T2 = typename Cplx<T>::type;
+  constexpr int NS = 3;  // one register slot per input: v, omega, phi
+  using St = Stage<R, T, W, NS, false>;
+  constexpr int ROWS = 64 * R;
+  constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
+  constexpr int NTAB = kspec_lds_tables_doubles<R, T, W>();
+  constexpr bool kDoubleTile = kspec_double_tile<R, T, W>();
+  constexpr int XS = xl_scratch_doubles(4);
+  __shared__ double tab_lds[TLDS ? NTAB : 1];
+  __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * St::TILE];
+  __shared__ double xs_mem[XM == kXlLds ? W * XS : 1];
+  const int lane = __lane_id();
+  const int w = threadIdx.x / 64;
+  const int N = a.N;
+  if (a.lds_poison) {
+    lds_poison_fill(tab_lds, sizeof(tab_lds));
+    lds_poison_fill(tile_mem, sizeof(tile_mem));
+    lds_poison_fill(xs_mem, sizeof(xs_mem));
+    __syncthreads();
+  }
+  if constexpr (TLDS) {
+    const double* src = tg.d1_lo;
+    for (int i = threadIdx.x; i < NTAB; i += W * 64) tab_lds[i] = src[i];
+  }
+  YTab t = tg;
+  auto fresh = [&]() {
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    if constexpr (TLDS) {
+      const double* b = tab_lds + z;
+      t.d1_lo = b + 0 * ROWS;
+      t.d1_up = b + 1 * ROWS;
+      t.d1_rm = b + 2 * ROWS;
+      t.d1_rc = b + 3 * ROWS;
+      t.d1_rp = b + 4 * ROWS;
+      t.d1fac = b + kYTabRowTables * ROWS;
+    } else {
+      t.d1_lo = tg.d1_lo + z;
+      t.d1_up = tg.d1_up + z;
+      t.d1_rm = tg.d1_rm + z;
+      t.d1_rc = tg.d1_rc + z;
+      t.d1_rp = tg.d1_rp + z;
+      t.d1fac = tg.d1fac + z;
+    }
+  };
+  for (int i = threadIdx.x; i < (kDoubleTile ? 2 : 1) * St::TILE; i += W * 64) tile_mem[i] = T2{0, 0};
+  __syncthreads();
+  const Xl<XM> xl{xs_mem + w * XS};
+  double* sred = reinterpret_cast<double*>(tile_mem);
+  static_assert(St::TILE * sizeof(T2) >= 4 * ROWS * sizeof(double), "tile too small for the statistics reduction");
+
+  const int ntiles = (a.lines + W - 1) / W;
+  const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
+  St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
+  st.set_layout(a.kzb, a.nkz);
+  const T2* vin = static_cast<const T2*>(a.out[1]);
+  const T2* omega = static_cast<const T2*>(a.omega);
+  const T2* phi = static_cast<const T2*>(a.phi);
+  // inputs: omega (slot 0), phi (slot 1), v (slot 2); each slot is refilled with the next tile's
+  // field right after its commit
+  if (lb < ntiles) {
+    st.template prefetch_at<0>(omega, lb * W);
+    st.template prefetch_at<2>(vin, lb * W);
+    st.template prefetch_at<1>(phi, lb * W);
+  }
+  for (int tile = lb; tile < ntiles; tile += gridDim.x) {
+    const int line0 = tile * W;
+    st.set_line0(line0);
+    const int line = line0 + w;
+    const bool valid = line < a.lines;
+    const int next_line0 = (tile + static_cast<int>(gridDim.x)) * W;
+    const bool has_next = next_line0 < a.lines;
+    const int ikx = valid ? line / a.nkz : 0;
+    const int kz = valid ? a.kz0 + (line - ikx * a.nkz) : 0;
+    const int ig = a.kx0 + ikx;
+    const int kx = ig <= a.Kx ? ig : ig - a.nkx;
+    const double al = a.ax * kx, be = a.az * kz;
+    const double k2 = al * al + be * be;
+    const bool is_mean = valid && kx == 0 && kz == 0;
+    const double inv_k2 = k2 > 0.0 ? 1.0 / k2 : 0.0;
+    const double mf = is_mean ? 1.0 : 0.0;
+    const double nz = (is_mean || k2 == 0.0) ? 0.0 : 1.0;
+
+    // vorticity first (it needs phi, D1 omega and v), then the velocities (D1 v and omega): two
+    // 2-RHS solves instead of one 4-RHS solve keep phi and D1 omega out of the velocity phase
+    double om[2][R], v[2][R], d[2][R], x[2][R];
+    st.template commit<0>(om);
+    if (has_next) st.template prefetch_at<0>(omega, next_line0);
+    fresh();
+    d1_apply_to<R, 2, XM>(t, om, d, xl, lane);  // D1 omega (mean line: dU/dy)
+    double dU0 = 0.0, dUN = 0.0;
+    if (a.mean_diag && is_mean) {
+      dU0 = row_value<R, XM>(d[0], 0, lane);
+      dUN = row_value<R, XM>(d[0], N - 1, lane);
+    }
+    st.template commit<2>(v);
+    if (has_next) st.template prefetch_at<2>(vin, next_line0);
+    {
+      double ph[2][R];
+      st.template commit<1>(ph);
+      if (has_next) st.template prefetch_at<1>(phi, next_line0);
+      // D2 v = phi + k2 v (Helmholtz identity); wx = Dw - i be v, wz = i al v - Du
+      // (convolution_kernels.cu:46-53), u, w from (nonLinear_kernels.cu:55-72)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double DDr = nz * ph[0][r] + k2 * v[0][r], DDi = nz * ph[1][r] + k2 * v[1][r];
+        const double br = (be * DDr + al * d[0][r]) * inv_k2, bi = (be * DDi + al * d[1][r]) * inv_k2;
+        x[0][r] = -bi + be * v[1][r];
+        x[1][r] = br - be * v[0][r];
+      }
+      st.store(static_cast<T2*>(a.out[3]), x[0], x[1]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double DDr = nz * ph[0][r] + k2 * v[0][r], DDi = nz * ph[1][r] + k2 * v[1][r];
+        const double ar = (al * DDr - be * d[0][r]) * inv_k2, ai = (al * DDi - be * d[1][r]) * inv_k2;
+        x[0][r] = -al * v[1][r] + ai - mf * d[0][r];
+        x[1][r] = al * v[0][r] - ar;
+      }
+      st.store(static_cast<T2*>(a.out[5]), x[0], x[1]);
+    }
+    fresh();
+    d1_apply_to<R, 2, XM>(t, v, d, xl, lane);  // D1 v
+    auto vel_u = [&](int r, double& re, double& im) {
+      const double ar = (al * d[0][r] - be * om[0][r]) * inv_k2, ai = (al * d[1][r] - be * om[1][r]) * inv_k2;
+      re = mf * om[0][r] - ai;  // mean line: U(y)
+      im = ar;
+    };
+    auto vel_w = [&](int r, double& re, double& im) {
+      const double br = (be * d[0][r] + al * om[0][r]) * inv_k2, bi = (be * d[1][r] + al * om[1][r]) * inv_k2;
+      re = -bi;
+      im = br;
+    };
+    if (a.stats) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) sred[i] = 0.0;
+      __syncthreads();
+      if (valid && !is_mean) {
+        const double wgt = kz == 0 ? 1.0 : 2.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int idx = r * 64 + lane;
+          double ur, ui, wr, wi;
+          vel_u(r, ur, ui);
+          vel_w(r, wr, wi);
+          atomicAdd(&sred[0 * ROWS + idx], wgt * (ur * ur + ui * ui));
+          atomicAdd(&sred[1 * ROWS + idx], wgt * (v[0][r] * v[0][r] + v[1][r] * v[1][r]));
+          atomicAdd(&sred[2 * ROWS + idx], wgt * (wr * wr + wi * wi));
+          atomicAdd(&sred[3 * ROWS + idx], wgt * (ur * v[0][r] + ui * v[1][r]));
+        }
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) {
+        const int s = i / ROWS, rem = i - s * ROWS, r = rem / 64, l = rem - r * 64;
+        const int j = l * R + r;
+        if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
+    st.store(static_cast<T2*>(a.out[0]), x[0], x[1]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
+    st.store(static_cast<T2*>(a.out[2]), x[0], x[1]);
+    if (a.out[4] != a.omega) st.store(static_cast<T2*>(a.out[4]), om[0], om[1], 1.0 - mf);
+    if (a.mean_diag && is_mean) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int j = lane * R + r;
+        if (j < N) a.mean_diag[j] = om[0][r];
+      }
+      if (lane == 0) {
+        a.mean_diag[3 * N + 0] = dU0;
+        a.mean_diag[3 * N + 1] = dUN;
+      }
+    }
+  }
+}
+
+// Split (advance kernel + output kernel), CHANNEL_KSPEC_SPLIT=1, at R = 5..7 (A/B; off by default:
+// at the headline grid the two kernels took 3.30 + 1.08 ms per substep against 4.17 ms fused, the
+// output kernel's 3 extra field reads costing more than its second wave per SIMD gains)
+static int kspec_split_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_SPLIT");
+    return e ? std::atoi(e) : -1;
+  }();
+  return v;
+}
+template <int R, typename T>
+constexpr bool kspec_split_default() {
+  // the instantiated split: fp32 storage, R = 5..7, where the output kernel is spill-free at two
+  // waves per SIMD (R = 8 and the fp64 slots spill at 256 VGPRs)
+  return sizeof(T) == 4 && R >= 5 && R <= 7;
+}
+template <int R, typename T>
+constexpr int kspec_out_lines() {
+  return 8;
+}
+
 // CHANNEL_KSPEC_GLDS7=1: the R = 7 fp32 kernel (headline grid) with async LDS staging instead of
 // its two register slots (A/B)
 static bool kspec_glds7() {
@@ -875,6 +1117,21 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
     if (kspec_ns7() == 3) kern = kspec_kernel<R, T, W, 3, kspec_xmode<R, T>(), PAR>;
+  }
+  const int sp = kspec_split_env();
+  if constexpr (kspec_split_default<R, T>()) {
+    if (sp == 1) {
+      auto k1 = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 0, 1>;
+      const int nt1 = (a.lines + W - 1) / W;
+      dim3 g1(std::min(nt1, resident_blocks(reinterpret_cast<const void*>(k1), W * 64))), b1(W * 64);
+      hipLaunchKernelGGL(k1, g1, b1, 0, stream, t.tab, a);
+      constexpr int W2 = kspec_out_lines<R, T>();
+      auto k2 = kspec_out_kernel<R, T, W2, kspec_xmode<R, T>()>;
+      const int nt2 = (a.lines + W2 - 1) / W2;
+      dim3 g2(std::min(nt2, resident_blocks(reinterpret_cast<const void*>(k2), W2 * 64))), b2(W2 * 64);
+      hipLaunchKernelGGL(k2, g2, b2, 0, stream, t.tab, a);
+      return;
+    }
   }
   // persistent grid: as many blocks as can be resident at once
   const int ntiles = (a.lines + W - 1) / W;

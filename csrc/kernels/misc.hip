@@ -55,28 +55,28 @@ void dt_update(const DtArgs& a, hipStream_t s) {
 // kz = 0 plane Hermitian symmetry q(-kx) = conj q(kx) for a field held entirely by one rank
 // (imposeSymetry.c:5-18 did this with a full FFT round trip).  lines are [y][kx][kz].
 template <typename T2>
-__global__ void symmetrize_kernel(T2* q, int N, int nkx, int nkz, int Kx) {
+__global__ void symmetrize_kernel(T2* q, int N, int nkx, int nkzs, int Kx, int kzb) {
   const int y = blockIdx.x;
   for (int i = threadIdx.x + 1; i <= Kx; i += blockDim.x) {
     const int im = nkx - i;  // index of -kx
-    T2* a = q + (static_cast<size_t>(y) * nkx + i) * nkz;
-    T2* b = q + (static_cast<size_t>(y) * nkx + im) * nkz;
+    T2* a = q + spec_index(kzb, N, nkx, nkzs, y, i, 0);
+    T2* b = q + spec_index(kzb, N, nkx, nkzs, y, im, 0);
     const T2 va = *a, vb = *b;
     const T2 m{static_cast<decltype(va.x)>(0.5 * (va.x + vb.x)), static_cast<decltype(va.x)>(0.5 * (va.y - vb.y))};
     *a = m;
     *b = T2{m.x, -m.y};
   }
   if (threadIdx.x == 0) {
-    T2* z = q + static_cast<size_t>(y) * nkx * nkz;
+    T2* z = q + spec_index(kzb, N, nkx, nkzs, y, 0, 0);
     z->y = 0;
   }
 }
 
-void symmetrize_kz0(void* q, int N, int nkx, int nkz, int Kx, bool fp64, hipStream_t s) {
+void symmetrize_kz0(void* q, int N, int nkx, int nkzs, int Kx, int kzb, bool fp64, hipStream_t s) {
   if (fp64)
-    hipLaunchKernelGGL(symmetrize_kernel<double2>, dim3(N), dim3(128), 0, s, static_cast<double2*>(q), N, nkx, nkz, Kx);
+    hipLaunchKernelGGL(symmetrize_kernel<double2>, dim3(N), dim3(128), 0, s, static_cast<double2*>(q), N, nkx, nkzs, Kx, kzb);
   else
-    hipLaunchKernelGGL(symmetrize_kernel<float2>, dim3(N), dim3(128), 0, s, static_cast<float2*>(q), N, nkx, nkz, Kx);
+    hipLaunchKernelGGL(symmetrize_kernel<float2>, dim3(N), dim3(128), 0, s, static_cast<float2*>(q), N, nkx, nkzs, Kx, kzb);
   HIP_LAUNCH_CHECK(s);
 }
 
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) spectra_kernel(SpectraArgs a) {
   double sx[3] = {0.0, 0.0, 0.0};
   for (int kl = threadIdx.x; kl < a.nkz_loc; kl += blockDim.x) {
     const int kz = a.kz0 + kl;
-    const size_t idx = static_cast<size_t>(j) * a.lines + static_cast<size_t>(ikx) * a.nkz_loc + kl;
+    const size_t idx = spec_index(a.kzb, a.N, a.nkx_loc, a.nkzs, j, ikx, kl);
     const double wgt = (kx == 0 && kz == 0) ? 0.0 : (kz == 0 ? 1.0 : 2.0);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {

@@ -58,12 +58,13 @@ def test_rollback_limit_then_abort(native):
         s.run(2, False)
 
 
-def _peer(rank, shm, q):
+def _peer(rank, shm, q, decomposition="slab"):
     os.environ["CHANNEL_COMM_TIMEOUT_S"] = "5"
     from channel_gpu_amd import require_native
 
     C = require_native()
-    s = C.Solver(default_config(**BASE, decomposition="slab"), rank, 2, 0, shm.encode())
+    s = C.Solver(default_config(**BASE, decomposition=decomposition, pr=2 if decomposition == "pencil" else 0),
+                 rank, 2, 0, shm.encode())
     s.init_ic()
     s.run(2, False)
     if rank == 1:
@@ -73,14 +74,19 @@ def _peer(rank, shm, q):
         s.run(5, False)
         q.put(("no-error", time.time() - t0))
     except RuntimeError as e:
-        q.put(("raised", time.time() - t0, str(e)))
+        t1 = time.time()
+        # every communicator (the pencil's per-axis groups too) was aborted: tearing the solver
+        # down must not block on the dead exchange
+        del s
+        q.put(("raised", t1 - t0, str(e), time.time() - t1))
 
 
-def test_dead_peer_raises_instead_of_hanging(native):
+@pytest.mark.parametrize("decomposition", ["slab", "pencil"])
+def test_dead_peer_raises_instead_of_hanging(native, decomposition):
     ctx = mpc.get_context("spawn")
     q = ctx.Queue()
     shm = f"shm:chfail_{uuid.uuid4().hex[:12]}"
-    ps = [ctx.Process(target=_peer, args=(r, shm, q)) for r in range(2)]
+    ps = [ctx.Process(target=_peer, args=(r, shm, q, decomposition)) for r in range(2)]
     for p in ps:
         p.start()
     res = q.get(timeout=240)
@@ -90,4 +96,5 @@ def test_dead_peer_raises_instead_of_hanging(native):
             p.kill()
     assert res[0] == "raised", res
     assert res[1] < 60
+    assert res[3] < 30, f"solver teardown took {res[3]:.1f} s after the failure"
     assert ps[1].exitcode == 3

@@ -198,3 +198,24 @@ def test_rccl_kspec_exchange_overlap_measured(native, monkeypatch):
     print("phase ms:", [round(x, 4) for x in ph])
     assert ph[0] > 0 and ph[4] > 0
     assert ph[7] > 0.0, "no K-SPEC / exchange overlap measured"
+
+
+def test_capture_failure_agreement_falls_back_eagerly(native, monkeypatch, capfd):
+    """A capture that fails on a rank (injected after the first substep has been recorded,
+    CHANNEL_TEST_CAPTURE_FAIL=<rank>) goes through the cross-rank capture agreement: the failed
+    capture is ended on every forked stream, the agreement allreduce runs on the communicator, and
+    the rank steps eagerly -- bitwise the captured run.  CHANNEL_MARKERS=1 prints the per-rank
+    progress lines bench.py enables at P > 1."""
+    monkeypatch.setenv("CHANNEL_MARKERS", "1")
+    ref = _run(native, native.new_unique_id(), nsteps=4, graph=True)
+    err = capfd.readouterr().err
+    assert ref[0].graph_active()
+    for m in ("eager warm-up step done", "step graph captured", "first replay of the step graph done"):
+        assert m in err, (m, err[-2000:])
+    monkeypatch.setenv("CHANNEL_TEST_CAPTURE_FAIL", "0")
+    got = _run(native, native.new_unique_id(), nsteps=4, graph=True)
+    err = capfd.readouterr().err
+    assert not got[0].graph_active()
+    assert "capture failure injected" in err and "step graph not captured" in err, err[-2000:]
+    assert _same(ref, got)
+    got[0].barrier()
