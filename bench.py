@@ -84,7 +84,7 @@ def main() -> None:
     ap.add_argument("--re", type=float, default=20700.0, help="1/nu (Re_tau~950 at Q=1.8, SURVEY App. C)")
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--decomposition", default="slab", choices=["slab", "pencil"])
-    ap.add_argument("--pr", type=int, default=0, help="pencil rows (0 = automatic, most square)")
+    ap.add_argument("--pr", type=int, default=0, help="pencil rows (0 = automatic: the fewest bytes on the busiest link, 4x2 at 8 ranks)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--phases", action="store_true",
                     help="after the timed steps, time a few more eagerly with per-phase hipEvents")

@@ -69,10 +69,25 @@ class SlabDecomposition:
         return 3 * 9 * worst
 
 
-def auto_pencil_grid(P: int) -> tuple[int, int]:
-    """Most square Pr x Pc with Pr <= Pc (Plan::auto_grid)."""
-    pr = max(r for r in range(1, int(P ** 0.5) + 1) if P % r == 0)
-    return pr, P // pr
+def auto_pencil_grid(P: int, NX: int, NY: int, NZ: int) -> tuple[int, int]:
+    """The Pr x Pc pencil grid (Pr, Pc > 1) with the fewest bytes on the busiest link
+    (Plan::auto_grid): per substep a rank sends (NY/Pc)(nkx/Pc)(nkz/Pr) complex values to each
+    column-group peer (A) and (NY/Pc)(NX/Pr)(nkz/Pr) to each row-group peer (B, x-expanded rows);
+    ties go to the squarer grid with Pr <= Pc.  (1, P) when P has no such factorisation."""
+    nkx, nkz = 2 * (NX // 3) + 1, (2 * NZ - 2) // 3 + 1
+    best, grid = None, (1, P)
+    for r in range(2, min(8, P - 1) + 1):
+        if P % r:
+            continue
+        c = P // r
+        if c > 8 or c > nkx or c > NY or r > nkz or r > NX:
+            continue
+        ny, kz = NY / c, nkz / r
+        link = max(ny * (nkx / c) * kz, ny * (NX / r) * kz)
+        squarer = abs(r - c) < abs(grid[0] - grid[1]) or (abs(r - c) == abs(grid[0] - grid[1]) and r <= c)
+        if best is None or link < best * (1 - 1e-9) or (link <= best * (1 + 1e-9) and squarer):
+            best, grid = link, (r, c)
+    return grid
 
 
 @dataclasses.dataclass(frozen=True)

@@ -64,7 +64,7 @@ struct Plan {
   // z-stage rows [y_loc][x_loc][kz] (pencil only; blocked by source kz range)
   size_t zrow_elems() const { return static_cast<size_t>(ny_loc) * nx_loc * nkz; }
   // automatic pencil grid: the most square Pr x Pc with Pr <= Pc
-  static void auto_grid(int P, int& Pr, int& Pc);
+  static void auto_grid(int P, int NX, int NY, int nkx, int nkz, int& Pr, int& Pc);
   // integer wavenumbers
   int kx_of(int i_global) const { return i_global <= Kx ? i_global : i_global - nkx; }
   // position of retained kx index in an NX-point FFT array

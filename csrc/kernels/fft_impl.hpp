@@ -71,6 +71,16 @@ static int fft_diag() {
   return d;
 }
 
+// blocked spectral layout: the wide x tiles as plane tiles (SL = 2); CHANNEL_XPLANES=0 keeps the
+// 8-column one-plane tiles (A/B)
+static bool xplanes_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_XPLANES");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 static bool xwide_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CHANNEL_XWIDE");
@@ -143,7 +153,10 @@ struct alignas(sizeof(T2) * V) CVec {
 // SM (kSegOne / kSegWin / kSegFull): how the kx source blocks are addressed; a per-element 8-way
 // compare/select lookup costs 22 chains per tile and spilled ~330 SGPRs
 // SL = 1: blocked spectral layout (XArgs::kzb, one rank: SM = kSegOne); tiles then walk y fastest,
-// so the tiles of one XCD share the 128-byte lines two planes of a kz block fill
+// so the tiles of one XCD share the 128-byte lines two planes of a kz block fill.  SL = 2: the
+// same layout with the C columns of a tile taken as C / 8 planes x one 8-wide kz block: each
+// retained kx then contributes one contiguous piece of C / 8 rows of the block (128 bytes, a whole
+// line, for the 16-column tiles) instead of 64-byte halves read by two tiles.
 template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
@@ -164,19 +177,22 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     __syncthreads();
   }
   for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
-  const int nkzc = (a.nkz + C - 1) / C;
-  const int ntiles = a.ny * nkzc * a.nfields;
+  // tile = YP planes x KC kz columns (column c: plane y0 + c / KC, kz kz0 + c % KC)
+  constexpr int KC = SL == 2 ? kSpecKzBlock : C, YP = C / KC;
+  static_assert(SL != 2 || C % kSpecKzBlock == 0, "plane tiles need whole kz blocks");
+  const int nkzc = (a.nkz + KC - 1) / KC, nyt = (a.ny + YP - 1) / YP;
+  const int ntiles = nyt * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
   const int nload = a.nkx * CW;
   CV v[EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
-  // tile t -> (f, y, kz0); at each iteration the blocks of one XCD take consecutive tiles
+  // tile t -> (f, y0, kz0); at each iteration the blocks of one XCD take consecutive tiles
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
-      y = t % a.ny;
-      const int rest = t / a.ny;
-      kz0 = (rest % nkzc) * C;
+      y = (t % nyt) * YP;
+      const int rest = t / nyt;
+      kz0 = (rest % nkzc) * KC;
       f = rest / nkzc;
     } else {
       kz0 = (t % nkzc) * C;
@@ -197,9 +213,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       // unconditional load from a clamped valid address: rows i >= nkx are never staged,
       // columns kz >= nkz are transformed (independently) but never stored
       const int i = min(e / CW, a.nkx - 1);
-      const int kz = min(kz0 + (e % CW) * V, a.nkz - V);
+      const int c = (e % CW) * V;
+      const int kz = min(kz0 + c % KC, a.nkz - V);
       if constexpr (SL) {
-        v[q] = *reinterpret_cast<const CV*>(base + spec_blk_off(a, y, i, kz));
+        v[q] = *reinterpret_cast<const CV*>(base + spec_blk_off(a, min(y + c / KC, a.ny - 1), i, kz));
       } else if constexpr (SM == kSegOne) {
         v[q] = *reinterpret_cast<const CV*>(
             base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
@@ -220,7 +237,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     decode(t, f, y, kz0);
     lds_barrier();  // previous tile's stores have finished reading s
     // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
-    // state, whose mean line holds U(y)); it is e = 0: thread 0, q = 0, u = 0
+    // state, whose mean line holds U(y)); it is kx row i = 0, the kz-0 column of each plane
     const bool zmean = f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
@@ -230,7 +247,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       if (e < nload)
 #pragma unroll
         for (int u = 0; u < V; ++u)
-          s[(c + u) * PITCH + fft_pidx(x)] = (q == 0 && u == 0 && zmean && e == 0) ? T2{0, 0} : v[q].c[u];
+          s[(c + u) * PITCH + fft_pidx(x)] = (zmean && i == 0 && (c + u) % KC == 0) ? T2{0, 0} : v[q].c[u];
     }
     // zero padding: only the band elements the first pass reads (its input blocks that straddle
     // the band edges; the blocks inside the band are compile-time zeros, wave_pass ZB)
@@ -263,16 +280,16 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     T2* out = phys + f * a.field_stride_phys;
     for (int e = tid; e < NX * CW; e += NT) {
       const int x = e / CW, c = (e - x * CW) * V;
-      const int kz = kz0 + c;
-      if (kz < a.nkz) {
+      const int kz = kz0 + c % KC, yy = y + c / KC;
+      if (kz < a.nkz && yy < a.ny) {
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SEG) {
           const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
-          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(y) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
+          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
         } else {
-          *reinterpret_cast<CV*>(out + static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) +
+          *reinterpret_cast<CV*>(out + static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
                                  static_cast<unsigned>(kz)) = w;
         }
       }
@@ -298,17 +315,19 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     __syncthreads();
   }
   for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
-  const int nkzc = (a.nkz + C - 1) / C;
-  const int ntiles = a.ny * nkzc * a.nfields;
+  constexpr int KC = SL == 2 ? kSpecKzBlock : C, YP = C / KC;
+  static_assert(SL != 2 || C % kSpecKzBlock == 0, "plane tiles need whole kz blocks");
+  const int nkzc = (a.nkz + KC - 1) / KC, nyt = (a.ny + YP - 1) / YP;
+  const int ntiles = nyt * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
   CV v[EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one destination block");
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
-      y = t % a.ny;
-      const int rest = t / a.ny;
-      kz0 = (rest % nkzc) * C;
+      y = (t % nyt) * YP;
+      const int rest = t / nyt;
+      kz0 = (rest % nkzc) * KC;
       f = rest / nkzc;
     } else {
       kz0 = (t % nkzc) * C;
@@ -325,14 +344,15 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
       const int x = min(e / CW, NX - 1);
-      const int kz = min(kz0 + (e % CW) * V, a.nkz - V);
+      const int c = (e % CW) * V;
+      const int kz = min(kz0 + c % KC, a.nkz - V), yy = min(y + c / KC, a.ny - 1);
       if constexpr (SEG) {
         const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
         v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(sp.off) +
-                                            static_cast<unsigned>(y * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) +
+                                            static_cast<unsigned>(yy * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) +
                                             static_cast<unsigned>(kz));
       } else {
-        v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(y * NX + x) * static_cast<unsigned>(a.nkz) +
+        v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
                                             static_cast<unsigned>(kz));
       }
     }
@@ -372,14 +392,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     for (int e0 = 0; e0 < a.nkx * CW; e0 += NT) {
       const int e = e0 + tid;
       const int i = e / CW, c = (e - i * CW) * V;
-      const int kz = kz0 + c;
-      if (e < a.nkx * CW && kz < a.nkz) {
+      const int kz = kz0 + c % KC, yy = y + c / KC;
+      if (e < a.nkx * CW && kz < a.nkz && yy < a.ny) {
         const int x = i <= a.Kx ? i : NX - (a.nkx - i);
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SL) {
-          *reinterpret_cast<CV*>(outb + spec_blk_off(a, y, i, kz)) = w;
+          *reinterpret_cast<CV*>(outb + spec_blk_off(a, yy, i, kz)) = w;
         } else if constexpr (SM == kSegOne) {
           *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
                                  static_cast<unsigned>(kz)) = w;
@@ -435,11 +455,13 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
   CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
            "xfft_backward: the blocked spectral layout needs one source block");
-  auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 1>
+  constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;  // blocked layout: plane tiles when wide
+  auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
               : a.npseg > 1   ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
                               : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
-  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
+  const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
 }
@@ -454,12 +476,14 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
   CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
            "xfft_forward: the blocked spectral layout needs one destination block");
-  auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, 1>
+  constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;
+  auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
               : a.npseg > 1           ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
               : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
                               : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;
-  const int ntiles = a.ny * ((a.nkz + Cfg::C - 1) / Cfg::C) * a.nfields;
+  const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
+  const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));
@@ -1156,7 +1180,7 @@ void fft_xb_len(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw,
   if (fp64) {
     xb_launch_cfg<NN, double, 0>(a, src, phys, tw, s);
   } else if constexpr (NN == 512 || NN == 1024) {
-    if (xwide_enabled()) xb_launch_cfg<NN, float, 1>(a, src, phys, tw, s);
+    if (xwide_enabled() || (a.kzb && xplanes_enabled())) xb_launch_cfg<NN, float, 1>(a, src, phys, tw, s);
     else xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
   } else {
     xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
@@ -1167,7 +1191,7 @@ void fft_xf_len(const XArgs& a, const void* phys, const XDst& dst, const Twiddle
   if (fp64) {
     xf_launch_cfg<NN, double, 0>(a, phys, dst, tw, s);
   } else if constexpr (NN == 512 || NN == 1024) {
-    if (xwide_enabled()) xf_launch_cfg<NN, float, 1>(a, phys, dst, tw, s);
+    if (xwide_enabled() || (a.kzb && xplanes_enabled())) xf_launch_cfg<NN, float, 1>(a, phys, dst, tw, s);
     else xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);
   } else {
     xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);

@@ -67,7 +67,7 @@ def test_a2a_volume_model():
 @pytest.mark.parametrize("P,pr", [(4, 2), (8, 2), (8, 4), (6, 3), (8, 0)])
 def test_pencil_plan_matches_python(native, P, pr):
     c = cfg(native, NX=1024, NY=385, NZ=513, decomposition="pencil", pr=pr)
-    Pr, Pc = (pr, P // pr) if pr else auto_pencil_grid(P)
+    Pr, Pc = (pr, P // pr) if pr else auto_pencil_grid(P, 1024, 385, 513)
     d = PencilDecomposition(1024, 385, 513, Pr, Pc)
     seen = set()
     for r in range(P):
@@ -124,3 +124,23 @@ def test_ny_cap_lifted_to_1536(native):
     assert native.Plan.make(cfg(native, NX=32, NY=1536, NZ=17), 1, 0).R == 24
     with pytest.raises(Exception, match="1536"):
         native.Plan.make(cfg(native, NX=32, NY=1537, NZ=17), 1, 0)
+
+
+def test_auto_pencil_grid_minimises_the_busiest_link():
+    """--decomposition pencil without pr/pc picks the factorisation with the fewest bytes on the
+    busiest link: 4 x 2 at 8 ranks of the headline grid (the B exchange carries x-expanded rows,
+    NX = 1.5 nkx, so the most square 2 x 4 loads a row-group link 1.5x more)."""
+    assert auto_pencil_grid(8, 1024, 385, 513) == (4, 2)
+    assert auto_pencil_grid(4, 1024, 385, 513) == (2, 2)
+    assert auto_pencil_grid(7, 1024, 385, 513) == (1, 7)
+    for P in (4, 6, 8):
+        Pr, Pc = auto_pencil_grid(P, 1024, 385, 513)
+        d = PencilDecomposition(1024, 385, 513, Pr, Pc)
+        link = max(max(d.exchange_bytes_per_substep(r)["A"] // max(1, Pc - 1),
+                       d.exchange_bytes_per_substep(r)["B"] // max(1, Pr - 1)) for r in range(P))
+        for r2 in range(2, P):
+            if P % r2 == 0 and r2 != Pr and P // r2 > 1:
+                d2 = PencilDecomposition(1024, 385, 513, r2, P // r2)
+                link2 = max(max(d2.exchange_bytes_per_substep(r)["A"] // max(1, P // r2 - 1),
+                                d2.exchange_bytes_per_substep(r)["B"] // max(1, r2 - 1)) for r in range(P))
+                assert link <= link2 * 1.01, (P, (Pr, Pc), (r2, P // r2))

@@ -12,7 +12,7 @@
 #   counters         rocprofv3 -L (available PMC counters) -> <TAG>_counter_names.txt
 #   configs          bench.py on every BASELINE config that fits one GPU
 #   rehearse2        2-rank torchrun bench on one GPU over the shared-memory loopback data plane
-#   rehearse8        8-rank bench.py --gpus 8 (slab, then pencil 2x4) over the loopback, headline grid
+#   rehearse8        8-rank bench.py --gpus 8 (slab, pencil 4x2 (auto), pencil 2x4) over the loopback, headline grid
 #   rehearse24       2- and 4-rank bench.py (slab, kx sub-block overlap) over the loopback, headline grid
 #   ab               bench.py once per env setting in AB_ENVS ("A=1 B=2;A=2 B=2")
 #   probe            transform stage alone (tools/xform_probe.py $PROBE_ARGS) per env setting in PROBE_ENVS
@@ -82,9 +82,11 @@ for step in "$@"; do
       tail -n 1 $log ;;
     rehearse8)
       # 8 ranks on the one GPU over the shared-memory loopback at the headline shape (bench.py
-      # self-launches torch.distributed.run): slab and the 2 x 4 pencil
-      for dec in slab pencil; do
-        CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus 8 --decomposition $dec --steps 2 --warmup 1 \
+      # self-launches torch.distributed.run): slab, the automatic pencil (4 x 2) and the 2 x 4 pencil
+      for dec in slab pencil pencil2x4; do
+        extra=""
+        [ $dec = pencil2x4 ] && extra="--decomposition pencil --pr 2" || extra="--decomposition $dec"
+        CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus 8 $extra --steps 2 --warmup 1 \
           $BENCH_ARGS > gpurun_out/${tag}_rehearse8_$dec.log 2>&1 || fail "rehearse8 $dec" gpurun_out/${tag}_rehearse8_$dec.log
         tail -n 1 gpurun_out/${tag}_rehearse8_$dec.log
       done ;;
