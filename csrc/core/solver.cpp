@@ -176,7 +176,7 @@ void Solver::alloc() {
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();
-  spec_ = static_cast<size_t>(p.NY) * p.nkx_loc * nkzs_;
+  spec_ = static_cast<size_t>(spec_rows(kzb_, p.NY)) * p.nkx_loc * nkzs_;
   physn_ = p.phys_elems();
   // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
   // every rank (a function of Pc and the environment), at most 8 exchange segments in total
@@ -340,7 +340,7 @@ size_t Solver::kb_index(int y, int ikx, int kz) const {
   return kb_off_[b] + (static_cast<size_t>(y) * kb_cnt_[b] + (ikx - kb_start_[b])) * plan_.nkz_loc + kz;
 }
 size_t Solver::dev_index(int y, int ikx, int kz) const {
-  if (kzb_) return spec_index(kzb_, plan_.NY, plan_.nkx_loc, nkzs_, y, ikx, kz);
+  if (kzb_) return spec_index(kzb_, plan_.nkx_loc, nkzs_, y, ikx, kz);
   return kb_index(y, ikx, kz);
 }
 
@@ -752,7 +752,6 @@ void Solver::transforms(int n, bool /*stats*/) {
     // address rows spec_y0 .. of the full fields
     xa.kzb = kzb_;
     xa.nkzs = nkzs_;
-    xa.spec_ny = p.NY;
     xa.spec_y0 = 0;
     XSrc src;
     src.base = out_;
@@ -1950,7 +1949,6 @@ Solver::Spectra Solver::spectra() {
   a.nkz_loc = p.nkz_loc;
   a.nkzs = nkzs_;
   a.kzb = kzb_;
-  a.N = p.NY;
   a.kz0 = p.kz0;
   a.nkx = p.nkx;
   a.Kx = p.Kx;

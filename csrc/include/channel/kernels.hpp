@@ -48,20 +48,33 @@ struct DenseD1Dev {
 void d1_dense_mfma(const DenseD1Dev& m, const void* in, void* out, int lines, hipStream_t stream);
 
 // ---- spectral field layout ----------------------------------------------------------------------
-// Element (y, local kx ikx, local kz) of a spectral field of nkx local kx and kz line stride nkzs
-// (a K-SPEC line is ikx * nkzs + kz).  kzb = 0: [y][kx][kz], every y plane contiguous (the exchange
-// blocks of P > 1 are row ranges).  kzb = 8 (one rank): [kz / 8][kx][y][kz % 8] with nkzs a
-// multiple of 8, so a block of 8 kz lines is one contiguous NY x 8 region: K-SPEC's tiles (4 lines
-// x all y) then read and write contiguous memory instead of 32-byte pieces one plane (~1.9 MB at
-// the headline grid) apart (tools/tilebench.hip: 2.5 -> 4.2 TB/s for that access pattern at
-// K-SPEC's occupancy); the x transforms still move 64-byte pieces (8 kz columns of one plane),
-// and the kx rows of one kz block stay within NX/1.5 * NY * 64 B (kz-block-major: a kx-major
-// block order spread one x-transform tile over the whole field).
-constexpr int kSpecKzBlock = 8;
-__host__ __device__ inline size_t spec_index(int kzb, int N, int nkx, int nkzs, int y, int ikx, int kz) {
-  return kzb ? (((static_cast<size_t>(kz / kSpecKzBlock) * nkx + ikx) * N + y) * kSpecKzBlock + kz % kSpecKzBlock)
-             : (static_cast<size_t>(y) * nkx + ikx) * nkzs + kz;
+// Element (y, line) of a spectral field, line = local kx * nkzs + local kz (nkzs: the kz line
+// stride), lines = nkx_loc * nkzs.  kzb = 0: [y][line], every y plane contiguous (the exchange
+// blocks of P > 1 are row ranges).  kzb = 8 (one rank, nkzs a multiple of 8, rows padded to a
+// multiple of 8): tiles of 8 planes x 8 kz lines, [y / 8][line / 8][y % 8][line % 8], i.e. a 512-B
+// (fp32) piece per (8-plane chunk, kz block).  The spectral fields are read in two shapes: K-SPEC
+// tiles (4 lines x all y: 49 such pieces instead of 385 rows of 32 B, 1.9 MB apart) and the
+// x transforms (2 planes x 8 kz x all kx: 128-B lines, the kx rows of one chunk 22 KB apart);
+// tools/tilebench.hip: K-SPEC's pattern 2.5 -> 4.2 TB/s blocked.  Blocking all NY rows of a kz
+// block instead ([kz/8][kx][y][8]) gave K-SPEC whole-tile contiguity but spread an x tile over
+// 16.8 MB and the chunk's tiles over the whole field: the x-backward's average read latency rose
+// from 950 to 1670 cycles (TCP_TCC_READ_REQ_LATENCY, gpurun_out/r4g*), 62 -> 71 us per chunk.
+// Row and line parts of the offset are separable: offset = spec_row_off(y) + spec_line_off(line),
+// and spec_row_off(y + 64) = spec_row_off(y) + 64 lines in both layouts.
+constexpr int kSpecKzBlock = 8, kSpecYBlock = 8;
+__host__ __device__ inline size_t spec_row_off(int kzb, int lines, int y) {
+  return kzb ? static_cast<size_t>(y / kSpecYBlock) * kSpecYBlock * lines + (y % kSpecYBlock) * kSpecKzBlock
+             : static_cast<size_t>(y) * lines;
 }
+__host__ __device__ inline size_t spec_line_off(int kzb, int line) {
+  return kzb ? static_cast<size_t>(line / kSpecKzBlock) * (kSpecYBlock * kSpecKzBlock) + line % kSpecKzBlock
+             : static_cast<size_t>(line);
+}
+__host__ __device__ inline size_t spec_index(int kzb, int nkx, int nkzs, int y, int ikx, int kz) {
+  return spec_row_off(kzb, nkx * nkzs, y) + spec_line_off(kzb, ikx * nkzs + kz);
+}
+// rows allocated per spectral field (kzb: whole 8-plane chunks)
+inline int spec_rows(int kzb, int N) { return kzb ? (N + kSpecYBlock - 1) / kSpecYBlock * kSpecYBlock : N; }
 
 // ---- the fused spectral (y-line) substep kernel ---------------------------------------------
 struct SpecArgs {
@@ -80,7 +93,7 @@ struct SpecArgs {
   // mean flow forcing
   double Q = 1.8;
   int forcing = 0;        // 0 implicit (exact flux), 1 parity (constant add)
-  // reference-parity switches (config influence / explicit_d2; NY <= 256)
+  // reference-parity switches (config influence / explicit_d2; every NY)
   bool explicit_dd = false;          // explicit viscous D2 = D1 o D1
   bool analytic_influence = false;   // cosh/sinh influence functions
   const double* ygrid = nullptr;     // [N] y_j (analytic influence)
@@ -158,8 +171,8 @@ struct XArgs {
   int kz_glob0 = 0;
   int lds_poison = 0;                // debug: fill the LDS with NaN before use
   // blocked spectral layout (one rank, one source block; spec_index with kzb = 8): rows spec_y0 ..
-  // spec_y0 + ny - 1 of fields of spec_ny rows and line stride nkzs
-  int kzb = 0, nkzs = 0, spec_ny = 0, spec_y0 = 0;
+  // spec_y0 + ny - 1 of fields of line stride nkzs (lines = nkx * nkzs)
+  int kzb = 0, nkzs = 0, spec_y0 = 0;
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
@@ -217,7 +230,7 @@ void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool
 struct SpectraArgs {
   const void *u = nullptr, *v = nullptr, *w = nullptr;  // spectral [NY][lines], lines = nkx_loc*nkz_loc
   int lines = 0, nkx_loc = 0, kx0 = 0, nkz_loc = 0, kz0 = 0;
-  int nkzs = 0, kzb = 0, N = 0;       // line stride in kz, layout (spec_index), NY
+  int nkzs = 0, kzb = 0;              // line stride in kz, layout (spec_index)
   int nkx = 0, Kx = 0, nkz = 0;       // global retained counts
   const int* planes = nullptr;        // device [nplanes] y indices
   int nplanes = 0;

@@ -131,11 +131,10 @@ inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
 }
 
 // element offset of (row y of the chunk, retained kx i, kz) in a blocked spectral field (spec_index
-// with kzb = 8; XArgs::spec_y0 / spec_ny / nkzs)
+// with kzb = 8; XArgs::spec_y0 / nkzs); consecutive kx rows are nkzs * 8 elements apart
 __device__ __forceinline__ unsigned spec_blk_off(const XArgs& a, int y, int i, int kz) {
-  const unsigned blk = static_cast<unsigned>((kz / kSpecKzBlock) * a.nkx + i);
-  return (blk * static_cast<unsigned>(a.spec_ny) + static_cast<unsigned>(a.spec_y0 + y)) * kSpecKzBlock +
-         static_cast<unsigned>(kz % kSpecKzBlock);
+  return static_cast<unsigned>(spec_row_off(kSpecKzBlock, a.nkx * a.nkzs, a.spec_y0 + y) +
+                               spec_line_off(kSpecKzBlock, i * a.nkzs + kz));
 }
 
 // V consecutive complex values moved by one global access (V = 2 for fp32: 16-byte loads and
@@ -205,6 +204,23 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     int f, y, kz0;
     decode(t, f, y, kz0);
     const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
+    if constexpr (SL) {
+      // each thread keeps one column (plane, kz) and walks kx rows i0 + q NT/CW, one block column
+      // stride apart; the retained kx count is NKMAX (checked on the host), so only the rows of the
+      // last accesses can pass it
+      static_assert(NT % CW == 0, "a thread's column must be the same for every access");
+      constexpr int DI = NT / CW;
+      const int c = (tid % CW) * V;
+      const T2* bt = base + spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V));
+      const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock;
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        int i = tid / CW + q * DI;
+        if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
+        v[q] = *reinterpret_cast<const CV*>(bt + static_cast<unsigned>(i) * rs);
+      }
+      return;
+    }
     // this rank's own block is read in place from its spectral field (no self exchange)
     const T2* sbase = src.self_seg >= 0 ? static_cast<const T2*>(src.self_base) + f * src.self_field_stride : base;
 #pragma unroll
@@ -215,9 +231,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int i = min(e / CW, a.nkx - 1);
       const int c = (e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V);
-      if constexpr (SL) {
-        v[q] = *reinterpret_cast<const CV*>(base + spec_blk_off(a, min(y + c / KC, a.ny - 1), i, kz));
-      } else if constexpr (SM == kSegOne) {
+      if constexpr (SM == kSegOne) {
         v[q] = *reinterpret_cast<const CV*>(
             base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
       } else {
@@ -387,6 +401,24 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    if constexpr (SL) {
+      // one column per thread (NT % CW == 0), kx rows one block-column stride apart
+      static_assert(NT % CW == 0, "a thread's column must be the same for every access");
+      const int c = (tid % CW) * V;
+      const int kz = kz0 + c % KC, yy = y + c / KC;
+      if (kz < a.nkz && yy < a.ny) {
+        T2* ot = outb + spec_blk_off(a, yy, 0, kz);
+        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock;
+        for (int i = tid / CW; i < a.nkx; i += NT / CW) {
+          const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(ot + static_cast<unsigned>(i) * rs) = w;
+        }
+      }
+      continue;
+    }
     // this rank's own block goes straight into its spectral field (no self exchange)
     T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
     for (int e0 = 0; e0 < a.nkx * CW; e0 += NT) {
@@ -398,9 +430,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-        if constexpr (SL) {
-          *reinterpret_cast<CV*>(outb + spec_blk_off(a, yy, i, kz)) = w;
-        } else if constexpr (SM == kSegOne) {
+        if constexpr (SM == kSegOne) {
           *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
                                  static_cast<unsigned>(kz)) = w;
         } else {
@@ -453,7 +483,7 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
   // its windows, computed up front, spilled ~640 SGPRs)
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
-  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
+  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0),
            "xfft_backward: the blocked spectral layout needs one source block");
   constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;  // blocked layout: plane tiles when wide
   auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
@@ -474,7 +504,7 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
     if (xvec_ok(a, dst.off, dst.ndst, dst.self_field_stride, 0)) return xf_launch_cfg<NN, T, WIDE, 2>(a, phys, dst, tw, s);
   }
   const int sm = seg_mode<Cfg::NT, Cfg::C / V>(dst.ndst, dst.kx_start, dst.self_seg, dst.off[0]);
-  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0 && a.spec_ny >= a.spec_y0 + a.ny),
+  CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0),
            "xfft_forward: the blocked spectral layout needs one destination block");
   constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;
   auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>

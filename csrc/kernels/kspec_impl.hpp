@@ -86,8 +86,9 @@ struct Stage {
   T2* tile;   // buffer of the last staging (column() reads it)
   T2* tile2;  // the other buffer (nullptr: single-buffered)
   int N, lines, line0, w, lane;
-  // spectral layout (spec_index): element (y, line) at lineoff(line) + y * rs
-  int kzb = 0, nkzs = 1, nkx = 1;
+  // spectral layout (spec_index): element (y, line) at rowoff(y) + lineoff(line); rows y and y + 64
+  // are 64 * rs = 64 * lines elements apart in either layout
+  int kzb = 0;
   unsigned rs = 0;
   // Per-thread element offset of (row y0 = tid / W, line line0 + tid % W) and of one 64-row pass:
   // re-derived per tile through an opaque copy, so the per-field addresses are formed at their
@@ -99,22 +100,15 @@ struct Stage {
   unsigned doff[kRegSlots || GL ? 1 : NS];
 
   static __device__ __forceinline__ int row_off(int y) { return y * PITCH + (G ? (y / R) : 0); }
-  __device__ __forceinline__ void set_layout(int kzb_, int nkzs_) {
+  __device__ __forceinline__ void set_layout(int kzb_) {
     kzb = kzb_;
-    nkzs = nkzs_;
-    nkx = lines / nkzs_;
-    rs = kzb ? static_cast<unsigned>(kSpecKzBlock) : static_cast<unsigned>(lines);
+    rs = static_cast<unsigned>(lines);
   }
-  __device__ __forceinline__ unsigned lineoff(int line) const {
-    if (!kzb) return static_cast<unsigned>(line);
-    const int ikx = line / nkzs, kz = line - ikx * nkzs;
-    return (static_cast<unsigned>(kz / kSpecKzBlock) * static_cast<unsigned>(nkx) + static_cast<unsigned>(ikx)) *
-               static_cast<unsigned>(N * kSpecKzBlock) +
-           static_cast<unsigned>(kz % kSpecKzBlock);
-  }
+  __device__ __forceinline__ unsigned lineoff(int line) const { return static_cast<unsigned>(spec_line_off(kzb, line)); }
+  __device__ __forceinline__ unsigned rowoff(int y) const { return static_cast<unsigned>(spec_row_off(kzb, lines, y)); }
   __device__ __forceinline__ unsigned thread_off(int l0) const {
     const int y0 = threadIdx.x / W, l = threadIdx.x % W;
-    unsigned o = static_cast<unsigned>(y0) * rs + lineoff(min(l0 + l, lines - 1));
+    unsigned o = rowoff(y0) + lineoff(min(l0 + l, lines - 1));
     asm volatile("" : "+v"(o));
     return o;
   }
@@ -145,7 +139,6 @@ struct Stage {
       constexpr int RPI = 64 / DPR;  // rows per instruction
       const int lane = __lane_id();
       const int ry = lane / DPR, dw = lane % DPR;
-      const unsigned stride = rs * DPE;  // dwords per global row
       const unsigned base = lineoff(min(l0 + dw / DPE, lines - 1)) * DPE + dw % DPE;
       const unsigned* srcd = reinterpret_cast<const unsigned*>(src);
       unsigned* dstd = reinterpret_cast<unsigned*>(tile2);
@@ -153,7 +146,7 @@ struct Stage {
       for (int k = w; k < ninst; k += W) {
         const int y = k * RPI + ry;
         if (y < N)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(srcd + (base + static_cast<unsigned>(y) * stride)),
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(srcd + (base + rowoff(y) * DPE)),
                                            (__attribute__((address_space(3))) void*)(dstd + 64 * k), 4, 0, 0);
       }
       (void)o;
@@ -163,7 +156,7 @@ struct Stage {
     } else {
       const int y0 = threadIdx.x / W, l = threadIdx.x % W;
       // rows >= N read row N-1 of the same (clamped) line
-      const unsigned last = static_cast<unsigned>(N - 1) * rs + lineoff(min(l0 + l, lines - 1));
+      const unsigned last = rowoff(N - 1) + lineoff(min(l0 + l, lines - 1));
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         const unsigned oq = y0 + RPB * q < N ? o + static_cast<unsigned>(RPB * q) * rs : last;
@@ -385,7 +378,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
-  st.set_layout(a.kzb, a.nkz);
+  st.set_layout(a.kzb);
   T2* phi = static_cast<T2*>(a.phi);
   T2* omega = static_cast<T2*>(a.omega);
   T2* Rphi = static_cast<T2*>(a.Rphi);
@@ -945,7 +938,7 @@ __global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) 
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
-  st.set_layout(a.kzb, a.nkz);
+  st.set_layout(a.kzb);
   const T2* vin = static_cast<const T2*>(a.out[1]);
   const T2* omega = static_cast<const T2*>(a.omega);
   const T2* phi = static_cast<const T2*>(a.phi);

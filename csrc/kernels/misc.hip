@@ -59,15 +59,15 @@ __global__ void symmetrize_kernel(T2* q, int N, int nkx, int nkzs, int Kx, int k
   const int y = blockIdx.x;
   for (int i = threadIdx.x + 1; i <= Kx; i += blockDim.x) {
     const int im = nkx - i;  // index of -kx
-    T2* a = q + spec_index(kzb, N, nkx, nkzs, y, i, 0);
-    T2* b = q + spec_index(kzb, N, nkx, nkzs, y, im, 0);
+    T2* a = q + spec_index(kzb, nkx, nkzs, y, i, 0);
+    T2* b = q + spec_index(kzb, nkx, nkzs, y, im, 0);
     const T2 va = *a, vb = *b;
     const T2 m{static_cast<decltype(va.x)>(0.5 * (va.x + vb.x)), static_cast<decltype(va.x)>(0.5 * (va.y - vb.y))};
     *a = m;
     *b = T2{m.x, -m.y};
   }
   if (threadIdx.x == 0) {
-    T2* z = q + spec_index(kzb, N, nkx, nkzs, y, 0, 0);
+    T2* z = q + spec_index(kzb, nkx, nkzs, y, 0, 0);
     z->y = 0;
   }
 }
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) spectra_kernel(SpectraArgs a) {
   double sx[3] = {0.0, 0.0, 0.0};
   for (int kl = threadIdx.x; kl < a.nkz_loc; kl += blockDim.x) {
     const int kz = a.kz0 + kl;
-    const size_t idx = spec_index(a.kzb, a.N, a.nkx_loc, a.nkzs, j, ikx, kl);
+    const size_t idx = spec_index(a.kzb, a.nkx_loc, a.nkzs, j, ikx, kl);
     const double wgt = (kx == 0 && kz == 0) ? 0.0 : (kz == 0 ? 1.0 : 2.0);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
