@@ -47,8 +47,9 @@ bool is_fp64_complex(const torch::Tensor& t) {
 struct YLineOps {
   YGrid grid;
   YTablesDev tab;
-  YLineOps(int NY, double stretch) : grid(YGrid::build(NY, stretch)) {
-    tab.upload(grid, yline_supported_R(NY), cur_stream());
+  YLineOps(int NY, double stretch, int halves) : grid(YGrid::build(NY, stretch)) {
+    // halves = 2: lines over two waves of R = 4 (K-SPEC's geometry for 258 < NY <= 512)
+    tab.upload(grid, halves == 2 ? 4 : yline_supported_R(NY), cur_stream(), halves);
   }
   torch::Tensor apply(int op, torch::Tensor in, py::object k2, double c) {
     check_dev_tensor(in, "in");
@@ -197,7 +198,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }
 
   py::class_<YLineOps>(m, "YLineOps")
-      .def(py::init<int, double>(), py::arg("NY"), py::arg("stretch") = 2.0)
+      .def(py::init<int, double, int>(), py::arg("NY"), py::arg("stretch") = 2.0, py::arg("halves") = 1)
       .def("apply", &YLineOps::apply, py::arg("op"), py::arg("x"), py::arg("k2") = py::none(), py::arg("c") = 0.0)
       .def("d1_mfma", &YLineOps::d1_mfma, py::arg("x"));
 

@@ -143,7 +143,11 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
       comm_row_ = comm_->group(row);
     }
   }
-  ytab_.upload(grid_, yline_supported_R(cfg_.NY), s_comp_);
+  {
+    int R = 1, H = 1;
+    kspec_geometry(cfg_.NY, fp64_, R, H);
+    ytab_.upload(grid_, R, s_comp_, H);
+  }
   tw_x_.build(plan_.NX, fp64_);
   tw_z_.build(plan_.Nzp, fp64_);
   alloc();

@@ -13,14 +13,19 @@ namespace channel {
 
 // R values the y-line kernels are instantiated for (64*R >= NY).
 int yline_supported_R(int NY);
+// K-SPEC line geometry for NY: R rows per lane on H waves per line (H = 2: lines over two waves,
+// 64 R H >= NY; CHANNEL_KSPEC_HALVES=0 keeps one wave per line)
+void kspec_geometry(int NY, bool fp64, int& R, int& H);
 
-// Device copies of the per-row coefficient tables (lane-major, see yline_device.hpp).
+// Device copies of the per-row coefficient tables (lane-major, see yline_device.hpp).  H = 2: row
+// j = h 64R + lane R + r of half h at index (h R + r) 64 + lane (a half's table is the one-wave
+// table of its rows), the D1 factorisation per half, and the halves' D1 spikes.
 struct YTablesDev {
   double* buf = nullptr;     // single allocation
   size_t bytes = 0;
   dev::YTab tab{};
-  int R = 1;
-  void upload(const YGrid& g, int R, hipStream_t stream);
+  int R = 1, H = 1;
+  void upload(const YGrid& g, int R, hipStream_t stream, int H = 1);
   void release();
   ~YTablesDev() { release(); }
 };

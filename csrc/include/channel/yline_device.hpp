@@ -236,6 +236,7 @@ struct YTab {
   const double* d1rowN;  // last row (wall derivative at y=+1)
   const double* d1fac;   // D1 factorisation table [nf][64]
   const double* trap;    // trapezoid weights (0 on padding; mean line only, never staged in LDS)
+  const double* d1spk;   // lines over two waves: this half's D1 spike (response to its coupling row)
   double w0[3], wN[3];   // D1 wall closures (w0[2], wN[2]: the third points, see d1_rhs)
   int N;
 };
@@ -246,6 +247,82 @@ constexpr int kYTabRowTables = 13;
 __device__ __forceinline__ double tab(const double* __restrict__ p, int r, int lane) {
   return p[r * 64 + lane];
 }
+
+// ---- lines over H waves ---------------------------------------------------------------------
+// H = 1: a line is one wave (lane l holds rows l R .. l R + R - 1).  H = 2: a line is two waves of
+// one workgroup, wave half h holding rows h HR + l R + r (HR = 64 R).  Every tridiagonal system is
+// solved per half with the coupling between rows HR - 1 and HR dropped (the per-wave SPIKE/PCR
+// solver below, unchanged), plus one extra right-hand side per half, the spike (the half's response
+// to its coupling coefficient); the halves then meet in a 2 x 2 interface solve (the two-partition
+// SPIKE form).  Stencils exchange one halo row per side, line sums add the two halves.  The two
+// waves of a line exchange values through a small LDS area with a per-line flag pair (no workgroup
+// barrier: only the partner is waited for, and line-dependent branches such as the mean line's stay
+// legal).  At NY = 385 this gives R = 4 (two waves per SIMD) instead of one wave of R = 7 per line.
+template <int H>
+struct LineG;
+template <>
+struct LineG<1> {
+  static constexpr int kH = 1;
+  int h = 0;
+};
+template <>
+struct LineG<2> {
+  static constexpr int kH = 2;
+  static constexpr int kXK = 16;  // doubles per exchange slot
+  int h = 0;
+  double* buf = nullptr;  // [2 parity][2 halves][kXK] of this line (LDS)
+  int* flag = nullptr;    // [2 halves] exchange generation of each half (LDS, zeroed at start)
+  mutable int gen = 0;
+  // uniform values of this half -> the partner's; the generation parity double-buffers the slots
+  // (a half can be at most one exchange ahead: it waits for the partner's flag of its generation)
+  // this half's slot of the next exchange: the caller's lanes write their values into it, then
+  // post() publishes them (the generation parity double-buffers the slots: a half can be at most
+  // one exchange ahead, it waits for the partner's flag of its generation)
+  __device__ __forceinline__ double* slot() const { return buf + (((gen + 1) & 1) * 2 + h) * kXK; }
+  // publish this half's slot, wait for the partner's; returns the partner's slot
+  __device__ __forceinline__ const double* post() const {
+    ++gen;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // every lane's slot writes first
+    if (__lane_id() == 0) __hip_atomic_store(flag + h, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // bounded wait (every wave must be able to finish: a broken pairing yields wrong results, which
+    // the oracle tests catch, never a hung kernel); the partner is normally a few hundred cycles away
+    for (int it = 0; it < (1 << 16) &&
+                     __hip_atomic_load(flag + (1 - h), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < gen;
+         ++it)
+      __builtin_amdgcn_s_sleep(1);
+    return buf + ((gen & 1) * 2 + (1 - h)) * kXK;
+  }
+  // wave-uniform values of this half -> the partner's
+  template <int K>
+  __device__ __forceinline__ void exch(const double (&mine)[K], double (&theirs)[K]) const {
+    static_assert(K <= kXK, "exchange slot too small");
+    double* sl = slot();
+    if (__lane_id() == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) sl[k] = mine[k];
+    const double* rb = post();
+#pragma unroll
+    for (int k = 0; k < K; ++k) theirs[k] = rb[k];
+  }
+};
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+// factorisation coefficients of one half: the lower coupling of the half's first row (row HR,
+// lane 0 of half 1) is dropped (the upper one of row HR - 1 drops out by itself: lane 63 has no
+// right neighbour in the wave)
+template <class Coef>
+struct CutLo {
+  const Coef& c;
+  bool cut;
+  __device__ void abc(int r, double& a, double& b, double& cc) const {
+    c.abc(r, a, b, cc);
+    if (cut && r == 0) a = 0.0;
+  }
+  __device__ double a(int r) const { return (cut && r == 0) ? 0.0 : c.a(r); }
+};
 
 // ---- factorisations: registers (k-dependent) or a 64-lane table (the constant D1) -------------
 // Per lane: the interior Thomas multipliers (inv, cp) of rows 0..R-2, the spikes Ls / Us (the
@@ -466,6 +543,88 @@ __device__ void psolve(const Fac& F, const Coef& coef, double (&d)[K][R], const 
   }
 }
 
+// ---- two-wave lines: spike right-hand side and interface -----------------------------------
+// this half's spike right-hand side: its coupling coefficient at its boundary row (half 0: the
+// upper coefficient of row HR - 1, lane 63; half 1: the lower coefficient of row HR, lane 0)
+template <int R, class Coef, class G>
+__device__ __forceinline__ void spike_rhs(double (&z)[R], const Coef& coef, const G& g, int lane) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) z[r] = 0.0;
+  if (g.h == 0) {
+    if (lane == 63) {
+      double a, b, c;
+      coef.abc(R - 1, a, b, c);
+      z[R - 1] = c;
+    }
+  } else if (lane == 0) {
+    z[0] = coef.a(0);
+  }
+}
+// rows 0 .. K-1 of d hold this half's local solutions, spk its spike: solve the 2 x 2 interface
+// system for x(HR - 1), x(HR) and subtract the spike times the partner's interface unknown.  Both
+// halves form the same numbers in the same order, so the interface values are bitwise shared.
+template <int R, int K, int KT, class G>
+__device__ void spike_join(double (&d)[KT][R], const double (&spk)[R], const G& g, int lane) {
+  static_assert(K <= KT, "rows");
+  if constexpr (G::kH == 2) {
+    static_assert(K + 1 <= LineG<2>::kXK, "exchange slot too small");
+    // the boundary lane writes its rows straight into the slot (no cross-lane broadcast)
+    double* mine = g.slot();
+    if (lane == (g.h == 0 ? 63 : 0)) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) mine[k] = g.h == 0 ? d[k][R - 1] : d[k][0];
+      mine[K] = g.h == 0 ? spk[R - 1] : spk[0];
+    }
+    const double* theirs = g.post();
+    const double ts = theirs[K], ms = mine[K];
+    const double v = g.h == 0 ? ms : ts, w = g.h == 0 ? ts : ms;
+    const double idet = 1.0 / (1.0 - v * w);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const double tk = theirs[k], mk = mine[k];
+      const double a0 = g.h == 0 ? mk : tk, b0 = g.h == 0 ? tk : mk;
+      const double xl = (a0 - v * b0) * idet;  // row HR - 1
+      const double xf = b0 - w * xl;           // row HR
+      const double cc = g.h == 0 ? xf : xl;
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[k][r] -= cc * spk[r];
+    }
+  }
+  (void)lane;
+}
+// 3-point stencils across the half boundary, in split phases so that the partner's latency hides
+// behind the stencil: stage (lane 0 publishes the half's first rows, lane 63 its last rows), the
+// stencil itself with zero neighbours at the half boundary (the in-wave shifts zero-fill), then
+// finish: row HR (lane 0 of half 1) adds its lower coefficient times the partner's last row, row
+// HR - 1 (lane 63 of half 0) its upper coefficient times the partner's first row.
+template <int R, int K, class G>
+__device__ __forceinline__ void halo_stage(const double (&x)[K][R], const G& g, int lane) {
+  if constexpr (G::kH == 2) {
+    static_assert(2 * K <= LineG<2>::kXK, "exchange slot too small");
+    double* mine = g.slot();
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) mine[k] = x[k][0];
+    if (lane == 63)
+#pragma unroll
+      for (int k = 0; k < K; ++k) mine[K + k] = x[k][R - 1];
+  }
+  (void)x, (void)lane;
+}
+template <int R, int K, class G>
+__device__ __forceinline__ void halo_finish(double (&out)[K][R], double a0, double cl, const G& g, int lane) {
+  if constexpr (G::kH == 2) {
+    const double* theirs = g.post();
+    if (g.h == 1 && lane == 0)
+#pragma unroll
+      for (int k = 0; k < K; ++k) out[k][0] += a0 * theirs[K + k];
+    if (g.h == 0 && lane == 63)
+#pragma unroll
+      for (int k = 0; k < K; ++k) out[k][R - 1] += cl * theirs[k];
+  }
+  (void)out, (void)a0, (void)cl, (void)lane;
+}
+
 // ---- stencils ----------------------------------------------------------------------------
 // value at global row j (wave-uniform j); returns 0 if j out of range
 template <int R, int XM>
@@ -480,15 +639,16 @@ __device__ __forceinline__ double row_value(const double (&x)[R], int j, int lan
 
 // out = tridiag(lo, c, up) * x with per-row tables (c = mask for M); cl, cc, cu scale the three
 // diagonals of a second table set added on top (fused (cA A + cB B) x, see apply_tri2)
-template <int R, int K, int XM>
+template <int R, int K, int XM, class G = LineG<1>>
 __device__ void apply_tri(const double* __restrict__ lo, const double* __restrict__ cc, const double* __restrict__ up,
-                          const double (&x)[K][R], double (&out)[K][R], int lane) {
+                          const double (&x)[K][R], double (&out)[K][R], int lane, const G& g = G{}) {
   double L[K], Rt[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     L[k] = shfl_up1<XM>(x[k][R - 1]);
     Rt[k] = shfl_dn1<XM>(x[k][0]);
   }
+  halo_stage<R, K>(x, g, lane);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const double a = tab(lo, r, lane), b = tab(cc, r, lane), c = tab(up, r, lane);
@@ -499,21 +659,23 @@ __device__ void apply_tri(const double* __restrict__ lo, const double* __restric
       out[k][r] = a * xm + b * x[k][r] + c * xp;
     }
   }
+  if constexpr (G::kH == 2) halo_finish<R, K>(out, tab(lo, 0, lane), tab(up, R - 1, lane), g, lane);
 }
 
 // out = (sA A + sB B) x for two tridiagonal table sets A = (alo, ac, aup), B = (blo, bc, bup)
 // (the explicit RK3 operator (1 - dt a nu k^2) M + dt a nu K in one pass, no M x / K x temporaries)
-template <int R, int K, int XM>
+template <int R, int K, int XM, class G = LineG<1>>
 __device__ void apply_tri2(const double* __restrict__ alo, const double* __restrict__ ac,
                            const double* __restrict__ aup, double sA, const double* __restrict__ blo,
                            const double* __restrict__ bc, const double* __restrict__ bup, double sB,
-                           const double (&x)[K][R], double (&out)[K][R], int lane) {
+                           const double (&x)[K][R], double (&out)[K][R], int lane, const G& g = G{}) {
   double L[K], Rt[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     L[k] = shfl_up1<XM>(x[k][R - 1]);
     Rt[k] = shfl_dn1<XM>(x[k][0]);
   }
+  halo_stage<R, K>(x, g, lane);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const double a = sA * tab(alo, r, lane) + sB * tab(blo, r, lane);
@@ -526,21 +688,27 @@ __device__ void apply_tri2(const double* __restrict__ alo, const double* __restr
       out[k][r] = a * xm + b * x[k][r] + c * xp;
     }
   }
+  if constexpr (G::kH == 2)
+    halo_finish<R, K>(out, sA * tab(alo, 0, lane) + sB * tab(blo, 0, lane), sA * tab(aup, R - 1, lane) + sB * tab(bup, R - 1, lane),
+                      g, lane);
 }
 
 // D1 right-hand side B1 f: the 3-point interior stencil with the one-sided wall closures folded
 // into rows 0 and N-1 of the tables; the closures' third points are f_2 (row 0: lane 0's own
 // register when R >= 3) and f_{N-3} (row N-1 at the wave-uniform slot rN: one scalar branch)
-template <int R, int K, int XM>
-__device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][R], int lane) {
-  apply_tri<R, K, XM>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane);
+template <int R, int K, int XM, class G = LineG<1>>
+__device__ void d1_rhs(const YTab& t, const double (&x)[K][R], double (&out)[K][R], int lane, const G& g = G{}) {
+  apply_tri<R, K, XM>(t.d1_rm, t.d1_rc, t.d1_rp, x, out, lane, g);
   const int N = t.N;
-  const int lN = (N - 1) / R, rN = (N - 1) - lN * R;  // wave-uniform
+  // row N - 1 in its half (two-wave lines: the host keeps rows N - 3 .. N - 1 in one half)
+  const int hN = (N - 1) / (64 * R), jN = (N - 1) - hN * 64 * R;
+  const int lN = jN / R, rN = jN - lN * R;  // wave-uniform
+  static_assert(G::kH == 1 || R >= 3, "two-wave lines need R >= 3");
   if constexpr (R >= 3) {
-    const double cp2 = lane == 0 ? t.w0[2] : 0.0;
+    const double cp2 = (lane == 0 && g.h == 0) ? t.w0[2] : 0.0;
 #pragma unroll
     for (int k = 0; k < K; ++k) out[k][0] += cp2 * x[k][2];
-    const double cm2 = lane == lN ? t.wN[2] : 0.0;
+    const double cm2 = (lane == lN && g.h == hN) ? t.wN[2] : 0.0;
     switch (rN) {
 #define CH_D1_RM2(RR)                                                                  \
   case RR:                                                                             \
@@ -601,24 +769,61 @@ __device__ __forceinline__ double wave_sum(double v) {
   wave_sum_n<1, XM>(a);
   return a[0];
 }
+// sums over the whole line (both halves, added in the same order in each)
+template <int K, int XM, class G>
+__device__ __forceinline__ void line_sum_n(double (&v)[K], const G& g) {
+  wave_sum_n<K, XM>(v);
+  if constexpr (G::kH == 2) {
+    double t[K];
+    g.template exch<K>(v, t);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = g.h == 0 ? v[k] + t[k] : t[k] + v[k];
+  }
+}
+template <int XM, class G>
+__device__ __forceinline__ double line_sum(double v, const G& g) {
+  double a[1] = {v};
+  line_sum_n<1, XM>(a, g);
+  return a[0];
+}
+// value at global row j of the line (wave-uniform j) in every lane of both halves
+template <int R, int XM, class G>
+__device__ __forceinline__ double line_row_value(const double (&x)[R], int j, const G& g, int lane) {
+  if constexpr (G::kH == 1) {
+    return row_value<R, XM>(x, j, lane);
+  } else {
+    const int hj = j / (64 * R);
+    double m[1] = {hj == g.h ? row_value<R, XM>(x, j - hj * 64 * R, lane) : 0.0}, t[1];
+    g.template exch<1>(m, t);
+    return hj == g.h ? m[0] : t[0];
+  }
+}
 
 // ---- operators on whole lines ------------------------------------------------------------
 // out = D1 x (compact first derivative): B1 x, then the constant factorisation from its table
-template <int R, int K, int XM>
+template <int R, int K, int XM, class G = LineG<1>>
 __device__ __forceinline__ void d1_apply_to(const YTab& t, const double (&x)[K][R], double (&out)[K][R],
-                                            const Xl<XM>& xl, int lane) {
-  d1_rhs<R, K, XM>(t, x, out, lane);
+                                            const Xl<XM>& xl, int lane, const G& g = G{}) {
+  d1_rhs<R, K, XM>(t, x, out, lane, g);
   const TFac<R> F{t.d1fac, lane};
   const CoefD1 cd{t, lane};
   psolve<R, K, XM>(F, cd, out, xl, lane);
+  if constexpr (G::kH == 2) {
+    double spk[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) spk[r] = tab(t.d1spk, r, lane);
+    spike_join<R, K, K>(out, spk, g, lane);
+  }
 }
-template <int R, int K, int XM>
-__device__ __forceinline__ void apply_M(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
-  apply_tri<R, K, XM>(t.m_lo, t.mask, t.m_up, x, o, lane);
+template <int R, int K, int XM, class G = LineG<1>>
+__device__ __forceinline__ void apply_M(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane,
+                                        const G& g = G{}) {
+  apply_tri<R, K, XM>(t.m_lo, t.mask, t.m_up, x, o, lane, g);
 }
-template <int R, int K, int XM>
-__device__ __forceinline__ void apply_K(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane) {
-  apply_tri<R, K, XM>(t.k_lo, t.k_c, t.k_up, x, o, lane);
+template <int R, int K, int XM, class G = LineG<1>>
+__device__ __forceinline__ void apply_K(const YTab& t, const double (&x)[K][R], double (&o)[K][R], int lane,
+                                        const G& g = G{}) {
+  apply_tri<R, K, XM>(t.k_lo, t.k_c, t.k_up, x, o, lane, g);
 }
 
 }  // namespace dev

@@ -71,13 +71,15 @@ constexpr bool kspec_glds_enabled() {
 // first field goes out after the output stores, which use both tiles; at R <= 8 the register
 // slots (two fields ahead, the next tile's issued during the D1 solve) measured faster
 // (profiles/r03s3/ab_kspec_glds_r7.txt).
-template <int R, typename T, int W, int NS, bool GL = false>
+// H = 2 (lines over two waves): the tile holds 64 R H rows, wave half h reads rows h 64R + lane R + r.
+template <int R, typename T, int W, int NS, bool GL = false, int H = 1>
 struct Stage {
   using T2 = typename Cplx<T>::type;
   static constexpr int PITCH = W + 1;
   static constexpr int G = (R * PITCH) % 2 == 1 ? 0 : 1;
-  static constexpr int TILE = 64 * R * PITCH + (G ? 64 : 0);
-  static constexpr int RPB = 64;  // rows per copy pass: W * 64 threads / W lines
+  static constexpr int TILE = 64 * R * H * PITCH + (G ? 64 * H : 0);
+  static constexpr int RPB = 64 * H;  // rows per copy pass: W * 64 H threads / W lines
+  static_assert(!GL || H == 1, "async LDS staging: one wave per line");
   static constexpr bool kRegSlots = R <= 8;
   static constexpr int DPE = static_cast<int>(sizeof(T2)) / 4;  // dwords per element
   static constexpr int DPR = W * DPE;                             // dwords per raw row
@@ -90,6 +92,7 @@ struct Stage {
   // are 64 * rs = 64 * lines elements apart in either layout
   int kzb = 0;
   unsigned rs = 0;
+  int h = 0;  // this wave's half of its line (H = 2)
   // Per-thread element offset of (row y0 = tid / W, line line0 + tid % W) and of one 64-row pass:
   // re-derived per tile through an opaque copy, so the per-field addresses are formed at their
   // use (a 64-bit field base + a 32-bit offset: global_load/store saddr forms) instead of being
@@ -202,7 +205,7 @@ struct Stage {
   // field, so a value just written out can be re-read from LDS (at storage precision) without
   // a global round trip, as long as no staging has happened since.
   __device__ __forceinline__ void column(double (&x)[2][R]) const {
-    const T2* c = tile + row_off(lane * R) + w;
+    const T2* c = tile + row_off(h * 64 * R + lane * R) + w;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const T2 v = c[r * PITCH];
@@ -221,7 +224,7 @@ struct Stage {
                                         double sc = 1.0) {
     next_tile();
     {
-      T2* c = tile + row_off(lane * R) + w;
+      T2* c = tile + row_off(h * 64 * R + lane * R) + w;
 #pragma unroll
       for (int r = 0; r < R; ++r) c[r * PITCH] = T2{static_cast<T>(sc * re[r]), static_cast<T>(sc * im[r])};
     }
@@ -255,26 +258,28 @@ __device__ __forceinline__ void chs_profiles(double l, double y, double& C, doub
 }
 
 // per-wave exchange scratch (kXlLds)
-template <int R, int W>
+template <int R, int W, int H = 1>
 constexpr int kspec_scratch_doubles() {
-  return kspec_xmode<R, float>() == kXlLds ? W * xl_scratch_doubles(kKspecXK) : 1;
+  return kspec_xmode<R, float>() == kXlLds ? W * H * xl_scratch_doubles(kKspecXK + (H == 2 ? 1 : 0)) : 1;
 }
-template <int R, typename T, int W>
+// staged tables: 13 row tables, the D1 factorisation (per half) and, for two halves, the D1 spikes
+template <int R, typename T, int W, int H = 1>
 constexpr int kspec_lds_tables_doubles() {
-  return kYTabRowTables * 64 * R + PFac<R>::kNumFields * 64;
+  return kYTabRowTables * 64 * R * H + PFac<R>::kNumFields * 64 * H + (H == 2 ? 64 * R * H : 0);
 }
 // stage the tables when tables + two tiles + the exchange scratch fit the 160 KB LDS
-template <int R, typename T, int W>
+template <int R, typename T, int W, int H = 1>
 constexpr bool kspec_tables_in_lds() {
-  return kspec_lds_tables_doubles<R, T, W>() * 8 + 2 * Stage<R, T, W, 1>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
-             kspec_scratch_doubles<R, W>() * 8 <=
+  return kspec_lds_tables_doubles<R, T, W, H>() * 8 +
+             2 * Stage<R, T, W, 1, false, H>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+             kspec_scratch_doubles<R, W, H>() * 8 <=
          158 * 1024;
 }
-template <int R, typename T, int W>
+template <int R, typename T, int W, int H = 1>
 constexpr bool kspec_double_tile() {
-  return (kspec_tables_in_lds<R, T, W>() ? kspec_lds_tables_doubles<R, T, W>() * 8 : 0) +
-             2 * Stage<R, T, W, 1>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
-             kspec_scratch_doubles<R, W>() * 8 <=
+  return (kspec_tables_in_lds<R, T, W, H>() ? kspec_lds_tables_doubles<R, T, W, H>() * 8 : 0) +
+             2 * Stage<R, T, W, 1, false, H>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+             kspec_scratch_doubles<R, W, H>() * 8 <=
          158 * 1024;
 }
 
@@ -291,22 +296,32 @@ constexpr int kParDD = 1, kParAnalytic = 2;
 // at R = 7, profiles/r03s3/ab_kspec_ns7.txt)
 // SPLIT: 0 = the whole substep in this kernel; 1 = stop after the phi / v stores (the D1 of v and
 // omega, the statistics and the u, w, omega_x, omega_z outputs run in kspec_out_kernel)
-template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0, int SPLIT = 0>
-__global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
+// H = 2: every line runs on two waves of the workgroup (LineG<2>, yline_device.hpp), waves 0 .. W-1
+// holding the first halves of the W lines and waves W .. 2W-1 the second halves
+template <int R, typename T, int W, int NS, int XM, int PAR, int GLM = 0, int SPLIT = 0, int H = 1>
+__global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
-  constexpr bool kGldsTile = (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
+  constexpr bool kGldsTile = H == 1 && (GLM == 1 || !Stage<R, T, W, 1>::kRegSlots) && Stage<R, T, W, 1>::kGldsOk &&
                              kspec_double_tile<R, T, W>() && kspec_glds_enabled();
-  using St = Stage<R, T, W, NS, kGldsTile>;
-  constexpr int ROWS = 64 * R;
-  constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
-  constexpr int NTAB = kspec_lds_tables_doubles<R, T, W>();
-  constexpr bool kDoubleTile = kspec_double_tile<R, T, W>();
-  constexpr int XS = xl_scratch_doubles(kKspecXK);
+  using St = Stage<R, T, W, NS, kGldsTile, H>;
+  constexpr int HR = 64 * R;        // rows of one wave
+  constexpr int ROWS = 64 * R * H;  // rows of a line (table stride)
+  constexpr int NT = W * 64 * H;
+  constexpr int NF = PFac<R>::kNumFields;
+  constexpr bool TLDS = kspec_tables_in_lds<R, T, W, H>();
+  constexpr int NTAB = kspec_lds_tables_doubles<R, T, W, H>();
+  constexpr bool kDoubleTile = kspec_double_tile<R, T, W, H>();
+  constexpr int XS = xl_scratch_doubles(kKspecXK + (H == 2 ? 1 : 0));  // (+ the spike column)
+  static_assert(H == 1 || (SPLIT == 0 && GLM == 0), "two-wave lines: the fused kernel");
   __shared__ double tab_lds[TLDS ? NTAB : 1];
   __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * St::TILE];
-  __shared__ double xs_mem[kspec_scratch_doubles<R, W>()];
+  __shared__ double xs_mem[kspec_scratch_doubles<R, W, H>()];
+  __shared__ double lx_buf[H == 2 ? W * 4 * LineG<2>::kXK : 1];
+  __shared__ int lx_flag[H == 2 ? W * 2 : 1];
   const int lane = __lane_id();
-  const int w = threadIdx.x / 64;
+  const int wv = threadIdx.x / 64;
+  const int w = wv % W;   // line slot of the tile
+  const int hh = wv / W;  // half of the line (H = 2)
   const int N = a.N;
   if (a.lds_poison) {
     lds_poison_fill(tab_lds, sizeof(tab_lds));
@@ -318,8 +333,17 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     // coefficient tables (13 per-row tables + the D1 factorisation, contiguous from d1_lo) staged
     // once per block: every solve step reads them, and from L2 each read is a dependent load
     const double* src = tg.d1_lo;
-    for (int i = threadIdx.x; i < NTAB; i += W * 64) tab_lds[i] = src[i];
+    for (int i = threadIdx.x; i < NTAB; i += NT) tab_lds[i] = src[i];
   }
+  LineG<H> g;
+  if constexpr (H == 2) {
+    g.h = hh;
+    g.buf = lx_buf + w * 4 * LineG<2>::kXK;
+    g.flag = lx_flag + w * 2;
+    if (threadIdx.x < W * 2) lx_flag[threadIdx.x] = 0;
+  }
+  // this half's rows: the half's table is the one-wave table of its rows (YTablesDev::upload)
+  const int thalf = hh * R * 64;
   // Table pointers re-derived at each phase from a laundered zero offset: the table reads are
   // loop-invariant, and without this LICM/GVN hoist every one of them out of the tile loop and
   // keep them live across all phases (13 tables x R + the D1 factor: ~260 registers at R = 7).
@@ -329,7 +353,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     int z = 0;
     asm volatile("" : "+v"(z));
     if constexpr (TLDS) {
-      const double* b = tab_lds + z;
+      const double* b = tab_lds + z + thalf;
       t.d1_lo = b + 0 * ROWS;
       t.d1_up = b + 1 * ROWS;
       t.d1_rm = b + 2 * ROWS;
@@ -343,29 +367,32 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       t.mask = b + 10 * ROWS;
       t.d1row0 = b + 11 * ROWS;
       t.d1rowN = b + 12 * ROWS;
-      t.d1fac = b + kYTabRowTables * ROWS;
+      const double* f = tab_lds + z + kYTabRowTables * ROWS;
+      t.d1fac = f + hh * NF * 64;
+      if constexpr (H == 2) t.d1spk = f + H * NF * 64 + thalf;
     } else {
-      t.d1_lo = tg.d1_lo + z;
-      t.d1_up = tg.d1_up + z;
-      t.d1_rm = tg.d1_rm + z;
-      t.d1_rc = tg.d1_rc + z;
-      t.d1_rp = tg.d1_rp + z;
-      t.m_lo = tg.m_lo + z;
-      t.m_up = tg.m_up + z;
-      t.k_lo = tg.k_lo + z;
-      t.k_c = tg.k_c + z;
-      t.k_up = tg.k_up + z;
-      t.mask = tg.mask + z;
-      t.d1row0 = tg.d1row0 + z;
-      t.d1rowN = tg.d1rowN + z;
-      t.d1fac = tg.d1fac + z;
+      t.d1_lo = tg.d1_lo + z + thalf;
+      t.d1_up = tg.d1_up + z + thalf;
+      t.d1_rm = tg.d1_rm + z + thalf;
+      t.d1_rc = tg.d1_rc + z + thalf;
+      t.d1_rp = tg.d1_rp + z + thalf;
+      t.m_lo = tg.m_lo + z + thalf;
+      t.m_up = tg.m_up + z + thalf;
+      t.k_lo = tg.k_lo + z + thalf;
+      t.k_c = tg.k_c + z + thalf;
+      t.k_up = tg.k_up + z + thalf;
+      t.mask = tg.mask + z + thalf;
+      t.d1row0 = tg.d1row0 + z + thalf;
+      t.d1rowN = tg.d1rowN + z + thalf;
+      t.d1fac = tg.d1fac + z + hh * NF * 64;
+      if constexpr (H == 2) t.d1spk = tg.d1spk + z + thalf;
     }
-    t.trap = tg.trap + z;  // (the mean line's weights: otherwise R 64-bit addresses live across the tile loop)
+    t.trap = tg.trap + z + thalf;  // (the mean line's weights: otherwise R 64-bit addresses live across the tile loop)
   };
   // zero tiles: rows >= N stay zero for the whole kernel (Stage::commit)
-  for (int i = threadIdx.x; i < (kDoubleTile ? 2 : 1) * St::TILE; i += W * 64) tile_mem[i] = T2{0, 0};
+  for (int i = threadIdx.x; i < (kDoubleTile ? 2 : 1) * St::TILE; i += NT) tile_mem[i] = T2{0, 0};
   __syncthreads();
-  const Xl<XM> xl{xs_mem + w * XS};
+  const Xl<XM> xl{xs_mem + wv * XS};
   // statistics reduction [4][64 R] in the staging tiles: between the phi store and the output
   // stores nothing reads them, and the output stores rewrite every slot a column read uses
   // (padding rows included, with zeros) before the next staging
@@ -379,6 +406,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
   st.set_layout(a.kzb);
+  st.h = hh;
+  // global row of (lane, r) in this wave
+  auto row = [&](int r) { return hh * HR + lane * R + r; };
   T2* phi = static_cast<T2*>(a.phi);
   T2* omega = static_cast<T2*>(a.omega);
   T2* Rphi = static_cast<T2*>(a.Rphi);
@@ -453,29 +483,29 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       {
         double X[2][R], G[2][R];
         {
-          double H[2][R];
-          st.template commit<0 % NS>(H);  // H_x
+          double Hc[2][R];
+          st.template commit<0 % NS>(Hc);  // H_x
           ahead(std::integral_constant<int, D>{}, line0);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            X[0][r] = al * H[1][r];  // -i al Hx
-            X[1][r] = -al * H[0][r];
-            G[0][r] = mf * H[0][r] - be * H[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
-            G[1][r] = be * H[0][r];
+            X[0][r] = al * Hc[1][r];  // -i al Hx
+            X[1][r] = -al * Hc[0][r];
+            G[0][r] = mf * Hc[0][r] - be * Hc[1][r];  // i be Hx ; mean line: N(y) = Re Hx(0,0)
+            G[1][r] = be * Hc[0][r];
           }
-          st.template commit<1 % NS>(H);  // H_z
+          st.template commit<1 % NS>(Hc);  // H_z
           ahead(std::integral_constant<int, 1 + D>{}, line0);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            X[0][r] += be * H[1][r];  // -i be Hz
-            X[1][r] -= be * H[0][r];
-            G[0][r] += al * H[1][r];  // -i al Hz
-            G[1][r] -= al * H[0][r];
+            X[0][r] += be * Hc[1][r];  // -i be Hz
+            X[1][r] -= be * Hc[0][r];
+            G[0][r] += al * Hc[1][r];  // -i al Hz
+            G[1][r] -= al * Hc[0][r];
           }
         }
         double Y[2][R];
         fresh();
-        d1_apply_to<R, 2, XM>(t, X, Y, xl, lane);  // D(-i al Hx - i be Hz)
+        d1_apply_to<R, 2, XM>(t, X, Y, xl, lane, g);  // D(-i al Hx - i be Hz)
         st.template commit<2 % NS>(X);              // H_y (X is free)
         ahead(std::integral_constant<int, 2 + D>{}, line0);
 #pragma unroll
@@ -483,8 +513,8 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
 #pragma unroll
           for (int r = 0; r < R; ++r) Y[k][r] -= k2 * X[k][r];
         fresh();
-        apply_M<R, 2, XM>(t, Y, RPn, lane);
-        apply_M<R, 2, XM>(t, G, RWn, lane);
+        apply_M<R, 2, XM>(t, Y, RPn, lane, g);
+        apply_M<R, 2, XM>(t, G, RWn, lane, g);
         KSPEC_STAMP(0)
         if (a.mean_diag && is_mean) {
           int z = 0;  // (laundered like the tables: keeps the addresses out of the loop preheader)
@@ -492,7 +522,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           double* md = a.mean_diag + N + z;
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            const int j = lane * R + r;
+            const int j = row(r);
             if (j < N) md[j] = G[0][r];
           }
         }
@@ -507,15 +537,15 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
             // reference parity (RK3_kernels.cu:160-164, derivatives_nu_double.cu:440-446): the
             // explicit viscous D2 of the fluctuations as D1 o D1, M (cM q + cK D1 D1 q)
             double D1q[2][R], DD[2][R];
-            d1_apply_to<R, 2, XM>(t, q, D1q, xl, lane);
-            d1_apply_to<R, 2, XM>(t, D1q, DD, xl, lane);
+            d1_apply_to<R, 2, XM>(t, q, D1q, xl, lane, g);
+            d1_apply_to<R, 2, XM>(t, D1q, DD, xl, lane, g);
 #pragma unroll
             for (int k = 0; k < 2; ++k)
 #pragma unroll
               for (int r = 0; r < R; ++r) DD[k][r] = cM * q[k][r] + cK * DD[k][r];
-            apply_M<R, 2, XM>(t, DD, o, lane);
+            apply_M<R, 2, XM>(t, DD, o, lane, g);
           } else {
-            apply_tri2<R, 2, XM>(t.m_lo, t.mask, t.m_up, cM, t.k_lo, t.k_c, t.k_up, cK, q, o, lane);
+            apply_tri2<R, 2, XM>(t.m_lo, t.mask, t.m_up, cM, t.k_lo, t.k_c, t.k_up, cK, q, o, lane, g);
           }
         };
         double q[2][R];
@@ -564,16 +594,18 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       {
         PFac<R> F;
         const CoefImpl ci{t, lane, 1.0 + c * k2, c};
-        pfactor<R, XM>(F, ci, xl, lane);
+        // (two-wave lines: each half factors its own rows, the coupling to the other half dropped)
+        pfactor<R, XM>(F, CutLo<CoefImpl>{ci, H == 2 && hh == 1 && lane == 0}, xl, lane);
+        constexpr int KS = H == 2 ? 1 : 0;  // + the half's spike right-hand side
         {
           // omega, phi and the two homogeneous phi solutions (k=0 -> phi(-1)=1, k=1 -> phi(+1)=1)
           // share the factorisation: one solve with 6 real right-hand sides
-          double Z[6][R];
+          double Z[6 + KS][R];
           int zl = 0;  // (laundered: the loop-invariant unit columns would otherwise be hoisted)
           asm volatile("" : "+v"(zl));
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            const int j = lane * R + r + zl;
+            const int j = row(r) + zl;
             Z[0][r] = rhsW[0][r];
             Z[1][r] = rhsW[1][r];
             Z[2][r] = rhsP[0][r];
@@ -581,7 +613,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
             Z[4][r] = (j == 0) ? 1.0 : 0.0;
             Z[5][r] = (j == N - 1) ? 1.0 : 0.0;
           }
-          psolve<R, 6, XM>(F, ci, Z, xl, lane);
+          if constexpr (H == 2) spike_rhs<R>(Z[6], ci, g, lane);
+          psolve<R, 6 + KS, XM>(F, ci, Z, xl, lane);
+          spike_join<R, 6, 6 + KS>(Z, Z[6 + KS - 1], g, lane);
 #pragma unroll
           for (int r = 0; r < R; ++r) {
             rhsW[0][r] = Z[0][r];
@@ -597,19 +631,21 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           double fU = 0.0;
 #pragma unroll
           for (int r = 0; r < R; ++r) fU += tab(t.trap, r, lane) * rhsW[0][r];
-          fU = wave_sum<XM>(fU);
+          fU = line_sum<XM>(fU, g);
           if (a.forcing == 0) {
-            double one[1][R], U1[1][R];
+            double one[1][R], U1[1 + KS][R];
             int zl = 0;  // (laundered: the loop-invariant 0/1 column would otherwise be hoisted)
             asm volatile("" : "+v"(zl));
 #pragma unroll
-            for (int r = 0; r < R; ++r) one[0][r] = (lane * R + r + zl < N) ? 1.0 : 0.0;
-            apply_tri<R, 1, XM>(t.m_lo, t.mask, t.m_up, one, U1, lane);
-            psolve<R, 1, XM>(F, ci, U1, xl, lane);
+            for (int r = 0; r < R; ++r) one[0][r] = (row(r) + zl < N) ? 1.0 : 0.0;
+            apply_tri<R, 1, XM>(t.m_lo, t.mask, t.m_up, one, reinterpret_cast<double (&)[1][R]>(U1), lane, g);
+            if constexpr (H == 2) spike_rhs<R>(U1[1], ci, g, lane);
+            psolve<R, 1 + KS, XM>(F, ci, U1, xl, lane);
+            spike_join<R, 1, 1 + KS>(U1, U1[KS], g, lane);
             double f1 = 0.0;
 #pragma unroll
             for (int r = 0; r < R; ++r) f1 += tab(t.trap, r, lane) * U1[0][r];
-            f1 = wave_sum<XM>(f1);
+            f1 = line_sum<XM>(f1, g);
             mean_C = f1 != 0.0 ? (a.Q - fU) / f1 : 0.0;
 #pragma unroll
             for (int r = 0; r < R; ++r) rhsW[0][r] += mean_C * U1[0][r];
@@ -633,10 +669,13 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       {
         PFac<R> F;
         const CoefHelm chm{t, lane, k2};
-        pfactor<R, XM>(F, chm, xl, lane);
-        double Y[4][R];  // v particular (0, 1), homogeneous v (2, 3)
-        apply_M<R, 4, XM>(t, pp, Y, lane);
-        psolve<R, 4, XM>(F, chm, Y, xl, lane);
+        pfactor<R, XM>(F, CutLo<CoefHelm>{chm, H == 2 && hh == 1 && lane == 0}, xl, lane);
+        constexpr int KS = H == 2 ? 1 : 0;
+        double Y[4 + KS][R];  // v particular (0, 1), homogeneous v (2, 3) [, the half's spike]
+        apply_M<R, 4, XM>(t, pp, reinterpret_cast<double (&)[4][R]>(Y), lane, g);
+        if constexpr (H == 2) spike_rhs<R>(Y[4], chm, g, lane);
+        psolve<R, 4 + KS, XM>(F, chm, Y, xl, lane);
+        spike_join<R, 4, 4 + KS>(Y, Y[4 + KS - 1], g, lane);
         fresh();
         // wall derivatives v'(+-1) = first / last row of the dense D1 applied to v (no solves)
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -652,7 +691,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           acc[6] += g0 * Y[3][r];
           acc[7] += gN * Y[3][r];
         }
-        wave_sum_n<8, XM>(acc);
+        line_sum_n<8, XM>(acc, g);
         const double p0r = acc[0], p0i = acc[1], pNr = acc[2], pNi = acc[3];
         double h10 = acc[4], h1N = acc[5], h20 = acc[6], h2N = acc[7];
         if ((PAR & kParAnalytic) && k2 > 0.0 && dt > 1e-14) {
@@ -676,7 +715,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
           h2N = dh[1][1];
 #pragma unroll
           for (int r = 0; r < R; ++r) {
-            const int j = lane * R + r;
+            const int j = row(r);
             const bool in = j < N;
             const double yj = in ? a.ygrid[j] : 0.0;
             double C1_, S1_, dC1, dS1, C2_, S2_, dC2, dS2;
@@ -731,10 +770,13 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       st.load(omega, om);
       PFac<R> F;
       const CoefHelm chm{t, lane, k2};
-      pfactor<R, XM>(F, chm, xl, lane);
-      double v[2][R];
-      apply_M<R, 2, XM>(t, ph, v, lane);
-      psolve<R, 2, XM>(F, chm, v, xl, lane);
+      pfactor<R, XM>(F, CutLo<CoefHelm>{chm, H == 2 && hh == 1 && lane == 0}, xl, lane);
+      constexpr int KS = H == 2 ? 1 : 0;
+      double v[2 + KS][R];
+      apply_M<R, 2, XM>(t, ph, reinterpret_cast<double (&)[2][R]>(v), lane, g);
+      if constexpr (H == 2) spike_rhs<R>(v[2], chm, g, lane);
+      psolve<R, 2 + KS, XM>(F, chm, v, xl, lane);
+      spike_join<R, 2, 2 + KS>(v, v[2 + KS - 1], g, lane);
       const double nz = (is_mean || k2 == 0.0) ? 0.0 : 1.0;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
@@ -774,7 +816,7 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     // ---------------- prepare velocity / vorticity for the physical-space stage --------------
     fresh();
     double dvo[4][R];  // D1 v (0, 1), D1 omega (2, 3): one 4-RHS solve
-    d1_apply_to<R, 4, XM>(t, vo, dvo, xl, lane);
+    d1_apply_to<R, 4, XM>(t, vo, dvo, xl, lane, g);
     KSPEC_STAMP(7)
     // velocities u = i (al dv - be om)/k2, w = i (be dv + al om)/k2 (nonLinear_kernels.cu:55-72),
     // formed one output at a time (each is stored before the next is built)
@@ -791,13 +833,13 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
     // plane statistics (statistics.cu:7-95), fluctuations only, weight 2 for kz > 0
     if (a.stats) {
       __syncthreads();  // every wave is done with the tiles (last staging: the phi store)
-      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) sred[i] = 0.0;
+      for (int i = threadIdx.x; i < 4 * ROWS; i += NT) sred[i] = 0.0;
       __syncthreads();
       if (valid && !is_mean) {
         const double wgt = kz == 0 ? 1.0 : 2.0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          const int idx = r * 64 + lane;
+          const int idx = (hh * R + r) * 64 + lane;
           double ur, ui, wr, wi;
           vel_u(r, ur, ui);
           vel_w(r, wr, wi);
@@ -808,9 +850,9 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
         }
       }
       __syncthreads();
-      for (int i = threadIdx.x; i < 4 * ROWS; i += W * 64) {
-        const int s = i / ROWS, rem = i - s * ROWS, r = rem / 64, l = rem - r * 64;
-        const int j = l * R + r;
+      for (int i = threadIdx.x; i < 4 * ROWS; i += NT) {
+        const int s = i / ROWS, rem = i - s * ROWS, hr = rem / 64, l = rem - hr * 64;
+        const int j = (hr / R) * HR + l * R + hr % R;
         if (j < N) atomicAdd(&a.stats[s * N + j], sred[i]);
       }
       __syncthreads();  // sred is a staging tile again
@@ -852,13 +894,13 @@ __global__ void __launch_bounds__(W * 64) kspec_kernel(YTab tg, SpecArgs a) {
       ostore(a.out[5], x[0], x[1]);
     }
     if (a.mean_diag && is_mean) {
-      const double d0 = row_value<R, XM>(dvo[2], 0, lane), dN = row_value<R, XM>(dvo[2], N - 1, lane);
+      const double d0 = line_row_value<R, XM>(dvo[2], 0, g, lane), dN = line_row_value<R, XM>(dvo[2], N - 1, g, lane);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int j = lane * R + r;
+        const int j = row(r);
         if (j < N) a.mean_diag[j] = vo[2][r];
       }
-      if (lane == 0) {
+      if (lane == 0 && hh == 0) {
         a.mean_diag[3 * N + 0] = d0;
         a.mean_diag[3 * N + 1] = dN;
         a.mean_diag[3 * N + 2] = mean_diag_flux;
@@ -1105,6 +1147,18 @@ static int kspec_ns7() {
 
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
+  if constexpr (R == 4 && sizeof(T) == 4) {
+    if (t.H == 2) {
+      // lines over two waves: 4 lines x 2 halves = 8 waves per workgroup (two per SIMD)
+      constexpr int W2 = 4;
+      auto k = kspec_kernel<4, float, W2, kspec_slots<4, float>(), kspec_xmode<4, float>(), PAR, 0, 0, 2>;
+      const int nt = (a.lines + W2 - 1) / W2;
+      dim3 grid(std::min(nt, resident_blocks(reinterpret_cast<const void*>(k), W2 * 128))), block(W2 * 128);
+      hipLaunchKernelGGL(k, grid, block, 0, stream, t.tab, a);
+      return;
+    }
+  }
+  CH_CHECK(t.H == 1, "kspec: lines over two waves are instantiated for R = 4, fp32 storage");
   constexpr int W = kspec_lines<R, T>();
   auto kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR>;
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {

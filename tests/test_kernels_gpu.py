@@ -43,6 +43,31 @@ def test_yline_operators(native, NY, dtype):
         assert e < t, f"op {op} NY={NY} {dtype}: rel err {e:.3e}"
 
 
+@pytest.mark.parametrize("NY", [259, 300, 385, 449, 512])
+@pytest.mark.parametrize("dtype", [torch.complex128, torch.complex64])
+def test_yline_operators_two_wave_lines(native, NY, dtype):
+    """The operators on lines over two waves (K-SPEC's geometry for 258 < NY <= 512): each half
+    solves locally with one spike right-hand side and the halves meet in the 2 x 2 interface solve;
+    stencils exchange one halo row per side.  Same tolerances as the one-wave operators."""
+    rng = np.random.default_rng(NY + 7)
+    L = 29
+    ops = ora.build_ops(NY)
+    x = rng.standard_normal((NY, L)) + 1j * rng.standard_normal((NY, L))
+    k2 = np.concatenate([[0.0], rng.uniform(0, 400.0, L - 1)])
+    c = 3e-3
+    Y = native.YLineOps(NY, 2.0, 2)
+    xt = torch.tensor(x, dtype=dtype, device=DEV)
+    k2t = torch.tensor(k2, dtype=torch.float64, device=DEV)
+    tol = 1e-10 if dtype == torch.complex128 else 2e-5
+    cases = {0: ora.op_d1(ops, x), 1: ora.op_helm(ops, x, k2), 2: ora.op_impl(ops, x, k2, c), 3: ora.op_M(ops, x),
+             4: ora.op_K(ops, x)}
+    for op, ref in cases.items():
+        got = Y.apply(op, xt, k2t, c).cpu().numpy()
+        e = rel(got, ref)
+        t = tol * (50 if (op == 1 and dtype == torch.complex64) else 1)
+        assert e < t, f"op {op} NY={NY} {dtype}: rel err {e:.3e}"
+
+
 @pytest.mark.parametrize("NY", [33, 65, 129, 192])
 def test_d1_dense_mfma(native, NY):
     """Dense D1 on the matrix cores (v_mfma_f64_16x16x4_f64) against the dense NumPy D1."""
