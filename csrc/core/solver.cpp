@@ -244,21 +244,21 @@ void Solver::alloc() {
   // on one stream); alternating two streams with 8-plane chunks: 50.6 ms/step.  The chunk is sized
   // in bytes (~144 MiB of x-expanded intermediates per stream), which the sweeps confirm across
   // grids: 512x257x512 best at 32 planes (11.2 -> 10.1 ms), 1024^2 fp64 at 4, 2048x633x2048 at 2
-  // (gpurun_out/yc_*, profiles/r01_v18_ychunk_sweep.log)
-  {
-    const size_t plane = 6ull * static_cast<size_t>(plan_.NX) * plan_.nkz * (fp64_ ? 16 : 8);
-    ychunk_ = static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, (144ull << 20) / plane)));
-  }
+  // (gpurun_out/yc_*, profiles/r01_v18_ychunk_sweep.log).  Two streams keep two chunks in flight,
+  // so at P = 1 each gets ~104 MiB (the pair stays inside the 256 MB cache): 6 planes at
+  // 1024x385x1024, 35.9 -> 35.2 ms/step (profiles/r04/ab_ychunk.txt)
   ystreams_ = 2;
-  // P > 1 slab: the same byte budget per chunk; each chunk is also one batched exchange per
-  // direction, so the exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms
-  // of chunk k
-  ychunk_p_ = ychunk_;
+  if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::max(1, std::min(8, std::atoi(ys)));
+  const size_t plane = 6ull * static_cast<size_t>(plan_.NX) * plan_.nkz * (fp64_ ? 16 : 8);
+  auto planes_in = [&](size_t mib) { return static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, (mib << 20) / plane))); };
+  ychunk_ = ystreams_ >= 2 ? std::max(2, planes_in(104)) : planes_in(144);  // (2048x633x2048: 2 planes, 300.8 vs 310.7 ms at 1)
+  // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
+  // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
+  ychunk_p_ = planes_in(144);
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
   // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
   if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
-  if (const char* ys = std::getenv("CHANNEL_YSTREAMS")) ystreams_ = std::max(1, std::min(8, std::atoi(ys)));
   for (int i = 2; i < ystreams_; ++i) {
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -1491,6 +1491,8 @@ void Solver::step(bool stats_for_next) {
       marker("eager warm-up step done (RCCL peers connected)");
     }
     if (captured_now) marker(gexec_[gi] ? "step graph captured" : "step graph not captured: stepping eagerly");
+    // eager steps (no graph, e.g. the host-driven loopback transport): one line per step issued
+    if (!done && !warmup_step) marker("eager step issued");
     if (done && !replayed_[gi]) {
       synchronize();
       replayed_[gi] = true;

@@ -83,7 +83,7 @@ for step in "$@"; do
     rehearse8)
       # 8 ranks on the one GPU over the shared-memory loopback at the headline shape (bench.py
       # self-launches torch.distributed.run): slab, the automatic pencil (4 x 2) and the 2 x 4 pencil
-      for dec in slab pencil pencil2x4; do
+      for dec in ${REHEARSE_DECS:-slab pencil pencil2x4}; do
         extra=""
         [ $dec = pencil2x4 ] && extra="--decomposition pencil --pr 2" || extra="--decomposition $dec"
         CHANNEL_COMM=shm timeout -k 10 600 python bench.py --gpus 8 $extra --steps 2 --warmup 1 \
