@@ -183,14 +183,14 @@ void Solver::alloc() {
   spec_ = static_cast<size_t>(spec_rows(kzb_, p.NY)) * p.nkx_loc * nkzs_;
   physn_ = p.phys_elems();
   // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
-  // every rank (a function of Pc and the environment), at most 8 exchange segments in total
+  // every rank (a function of Pc and the environment), at most kMaxSeg exchange segments in total
   nkb_ = 1;
   if (comm_) {  // (pencil: the column group's A exchange, kx <-> y, is the slab's)
-    int want = p.Pc <= 2 ? 4 : (p.Pc <= 4 ? 2 : 1);
+    int want = p.Pc <= 2 ? 4 : 2;
     if (const char* e = std::getenv("CHANNEL_KBLOCKS")) want = std::atoi(e);
     int minc = p.nkx;
     for (int c = 0; c < p.Pc; ++c) minc = std::min(minc, p.kx_split.count[c]);
-    nkb_ = std::max(1, std::min({want, 8 / p.Pc, minc}));
+    nkb_ = std::max(1, std::min({want, kMaxSeg / p.Pc, minc}));
     // the round-1 per-field pencil exchange (A/B) addresses whole rank blocks
     if (p.pencil() && std::getenv("CHANNEL_PENCIL_UNCHUNKED")) nkb_ = 1;
   }
@@ -202,6 +202,11 @@ void Solver::alloc() {
     for (int b = 1; b < nkb_; ++b) kb_off_[b] = kb_off_[b - 1] + static_cast<size_t>(p.NY) * kb_cnt_[b - 1] * p.nkz_loc;
     ev_kb_.resize(nkb_);
     for (auto& e : ev_kb_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev_fb_.resize(nkb_);
+    for (auto& e : ev_fb_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_cfl_, hipEventDisableTiming));
+    // CHANNEL_FWD_SPLIT=0: the whole forward exchange completes before K-SPEC (A/B)
+    if (const char* e = std::getenv("CHANNEL_FWD_SPLIT")) fwd_split_ = std::atoi(e) != 0;
   }
   xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz_loc;
   zstride_ = p.pencil() ? p.zrow_elems() : 0;
@@ -299,9 +304,10 @@ void Solver::free_all() {
   for (auto st : s_extra_) (void)hipStreamDestroy(st);
   ev_join_.clear();
   s_extra_.clear();
-  for (auto* v : {&ev_cb_, &ev_cc_, &ev_kb_})
+  for (auto* v : {&ev_cb_, &ev_cc_, &ev_kb_, &ev_fb_})
     for (auto e : *v) (void)hipEventDestroy(e);
   ev_kb_.clear();
+  ev_fb_.clear();
   for (auto& v : ev_pen_) {
     for (auto e : v) (void)hipEventDestroy(e);
     v.clear();
@@ -314,7 +320,7 @@ void Solver::free_all() {
   ev_cb_.clear();
   ev_cc_.clear();
   step_ev_.clear();
-  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_stats_, ev_tdt_[0], ev_tdt_[1]})
+  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_cfl_, ev_stats_, ev_tdt_[0], ev_tdt_[1]})
     if (e) (void)hipEventDestroy(e);
   if (h_tdt_) (void)hipHostFree(h_tdt_);
   h_tdt_ = nullptr;
@@ -561,11 +567,13 @@ void Solver::kspec(int mode, int n, bool stats) {
   // (measured r2s: splitting this fused pass into an advance kernel and a prepare kernel frees no
   // occupancy at R = 7 -- 481 and 348 registers -- and costs 10.2 vs 7.2 ms per substep)
   if (nkb_ == 1) {
+    join_forward();
     kspec_launch(ytab_, a, fp64_, s_comp_);
   } else {
     // kx sub-block b: the lines of local kx [kb_start_[b], +kb_cnt_[b]), a [y][lines_b] region of
     // every field; ev_kb_[b] lets the comm stream send block b while block b+1 is solved
     for (int b = 0; b < nkb_; ++b) {
+      if (fwd_pending_) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fb_[b], 0));  // block b's returned rows
       SpecArgs ab = a;
       const size_t off = kb_off_[b] * esz_;
       auto sh = [&](void* q) { return static_cast<void*>(static_cast<char*>(q) + off); };
@@ -580,6 +588,7 @@ void Solver::kspec(int mode, int n, bool stats) {
       kspec_launch(ytab_, ab, fp64_, s_comp_);
       HIP_CHECK(hipEventRecord(ev_kb_[b], s_comp_));
     }
+    fwd_pending_ = false;  // (the last wait joined the comm stream's forward exchange back)
   }
   ev(0, true);
   if (stats && comm_) {
@@ -1029,7 +1038,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   xa.field_stride_spec = static_cast<long long>(xstride_);
   // exchange segments: block b of rank c is segment c * nkb_ + b (global kx order)
   const int NB = nkb_, NS = P * NB;
-  CH_CHECK(NS <= 8, "at most 8 exchange segments");
+  CH_CHECK(NS <= kMaxSeg, "at most " << kMaxSeg << " exchange segments");
   XSrc src;
   src.base = xbuf_;
   src.nsrc = NS;
@@ -1058,6 +1067,8 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   const bool present = NB > 1 && n == 0 && presend_done_;  // blocks 0 .. NB-2 already sent
   presend_done_ = false;
   const int bchunk = (overlap || present) ? NB - 1 : 0;  // blocks still to send per chunk: [bchunk, NB)
+  const bool fsplit = NB > 1 && fwd_split_;
+  join_forward();  // (normally consumed by the K-SPEC in between)
   if (overlap) {
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
@@ -1110,17 +1121,39 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     }
     HIP_CHECK(hipEventRecord(ev_cc_[k], s_comp_));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_cc_[k], 0));
+    if (fsplit && k == nch - 1) {
+      // forward-path overlap: the CFL maxima first (every z stage is done), then the last chunk's
+      // rows block by block; K-SPEC block b waits only for ev_fb_[b] (kspec())
+      if (n == 0) {
+        ev(5, false, s_comm_);
+        comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+        ev(5, true, s_comm_);
+        HIP_CHECK(hipEventRecord(ev_cfl_, s_comm_));
+      }
+      for (int b = 0; b < NB; ++b) {
+        ev(4, false, s_comm_);
+        a2a_slab_rows(k * ch, ch, false, 3, b, b + 1);
+        ev(4, true, s_comm_);
+        HIP_CHECK(hipEventRecord(ev_fb_[b], s_comm_));
+      }
+      continue;
+    }
     ev(4, false, s_comm_);
     a2a_slab_chunk(k, ch, false, 3);
     ev(4, true, s_comm_);
   }
-  if (n == 0) {  // every chunk's z stage precedes ev_cc_[nch-1], which the comm stream waited on
-    ev(5, false, s_comm_);
-    comm_->allreduce_max_f32(d_max_, 4, s_comm_);
-    ev(5, true, s_comm_);
+  if (fsplit) {
+    if (n == 0) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_cfl_, 0));
+    fwd_pending_ = true;
+  } else {
+    if (n == 0) {  // every chunk's z stage precedes ev_cc_[nch-1], which the comm stream waited on
+      ev(5, false, s_comm_);
+      comm_->allreduce_max_f32(d_max_, 4, s_comm_);
+      ev(5, true, s_comm_);
+    }
+    HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
   }
-  HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
-  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fwd_done_, 0));
   if (n == 0) dt_update(da, s_comp_);
   roctxRangePop();
 }
@@ -1196,7 +1229,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
   xa.x_start[Pr] = p.NX;
   // A-exchange segments: kx sub-block b of column c is segment c * nkb_ + b (global kx order)
   const int NB = nkb_, NSG = Pc * NB;
-  CH_CHECK(NSG <= 8, "at most 8 exchange segments");
+  CH_CHECK(NSG <= kMaxSeg, "at most " << kMaxSeg << " exchange segments");
   XSrc src;
   src.base = xbuf_;
   src.nsrc = NSG;
@@ -1379,6 +1412,7 @@ void Solver::marker(const char* what) {
 // left in capture mode (a later collective on such a stream would fail on this rank only and strand
 // its peers in the capture agreement below).
 void Solver::end_failed_capture() {
+  fwd_pending_ = false;  // (the captured forward exchange is discarded with the graph)
   hipGraph_t junk = nullptr;
   (void)hipStreamEndCapture(s_comp_, &junk);
   if (junk) (void)hipGraphDestroy(junk);
@@ -1511,7 +1545,17 @@ void Solver::substep_debug(int n) {
   kspec(1, n, false);
 }
 
-void Solver::transforms_debug(bool dt_upd) { transforms(dt_upd ? 0 : 1, false); }
+void Solver::transforms_debug(bool dt_upd) {
+  transforms(dt_upd ? 0 : 1, false);
+  join_forward();
+}
+
+// the compute stream waits for every block of a split forward exchange (no K-SPEC follows)
+void Solver::join_forward() {
+  if (!fwd_pending_) return;
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_fb_.back(), 0));
+  fwd_pending_ = false;
+}
 
 // P > 1: poll instead of blocking so that a dead or hung peer (RCCL async error, or no progress
 // for CHANNEL_COMM_TIMEOUT_S seconds) aborts the communicator and raises on every surviving rank

@@ -137,11 +137,13 @@ struct Twiddles {
 // Blocks self_seg .. self_seg + nself - 1 (this rank's own kx range, if self_seg >= 0; several when
 // the rank's spectral fields are stored as kx sub-blocks, Solver::nkb_) live at self_base + f *
 // self_field_stride + off[s] instead (the spectral field itself: no self exchange, no copy).
+// exchange segments of the x transforms: P ranks x kx sub-blocks (slab8 with 2 sub-blocks: 16)
+constexpr int kMaxSeg = 16;
 struct XSrc {
   const void* base = nullptr;
   int nsrc = 1;
-  int kx_start[9] = {0};   // global retained-kx start of source s (kx_start[nsrc] = nkx)
-  long long off[8] = {0};  // element offset of source block s
+  int kx_start[kMaxSeg + 1] = {0};   // global retained-kx start of source s (kx_start[nsrc] = nkx)
+  long long off[kMaxSeg] = {0};      // element offset of source block s
   int self_seg = -1;
   int nself = 1;
   const void* self_base = nullptr;
@@ -150,8 +152,8 @@ struct XSrc {
 struct XDst {             // destination blocks for the forward x-transform (per destination rank)
   void* base = nullptr;
   int ndst = 1;
-  int kx_start[9] = {0};
-  long long off[8] = {0};
+  int kx_start[kMaxSeg + 1] = {0};
+  long long off[kMaxSeg] = {0};
   int self_seg = -1;
   int nself = 1;
   void* self_base = nullptr;
@@ -226,7 +228,7 @@ void symmetrize_kz0(void* q, int N, int nkx, int nkzs, int Kx, int kzb, bool fp6
 struct Kz0SymArgs {
   int N = 0, nkx_loc = 0, nkz_loc = 0, kx0 = 0, nkx = 0;
   int nblk = 1;
-  int kx_start[9] = {0};
+  int kx_start[kMaxSeg + 1] = {0};
 };
 void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp64, hipStream_t s);
 void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool fp64, hipStream_t s);

@@ -252,6 +252,13 @@ class Solver {
   // the step.  presend_done_: that exchange has been issued for the next substep 0.
   bool presend_done_ = false;
   bool kb_overlap() const { return nkb_ > 1 && comm_ != nullptr; }
+  // Forward-path overlap (slab, kx sub-blocks): the last y chunk's forward exchange goes out block
+  // by block (ev_fb_[b] on the comm stream) and K-SPEC block b waits only for block b's rows.
+  // fwd_pending_: the next kspec() (or join_forward()) must consume those events.
+  std::vector<hipEvent_t> ev_fb_;
+  hipEvent_t ev_cfl_ = nullptr;
+  bool fwd_split_ = true, fwd_pending_ = false;
+  void join_forward();
   void presend_backward(bool wait_blocks);
   int kb_gstart(int c, int b) const;       // global retained-kx start of block b of column rank c
   int kb_gcount(int c, int b) const;

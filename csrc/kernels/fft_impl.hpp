@@ -235,8 +235,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         v[q] = *reinterpret_cast<const CV*>(
             base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
       } else {
-        const SegPos sp = SM == kSegWin ? seg_find_win(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
-                                        : seg_find(src.kx_start, src.off, src.nsrc, i);
+        const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
+                                        : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
         const T2* b = static_cast<unsigned>(sp.idx - src.self_seg) < static_cast<unsigned>(src.nself) ? sbase : base;
         // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
         v[q] = *reinterpret_cast<const CV*>(
@@ -434,8 +434,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
                                  static_cast<unsigned>(kz)) = w;
         } else {
-          const SegPos sp = SM == kSegWin ? seg_find_win(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
-                                          : seg_find(dst.kx_start, dst.off, dst.ndst, i);
+          const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
+                                          : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
           T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
           *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz) = w;
         }

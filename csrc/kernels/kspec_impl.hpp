@@ -103,6 +103,14 @@ struct Stage {
   unsigned doff[kRegSlots || GL ? 1 : NS];
 
   static __device__ __forceinline__ int row_off(int y) { return y * PITCH + (G ? (y / R) : 0); }
+  // row of this thread in a copy pass, laundered like toff: the per-q row masks and clamped offsets
+  // derived from it are loop invariants the compiler would otherwise keep live (or spill) across
+  // the whole tile loop
+  static __device__ __forceinline__ int copy_row() {
+    int y0 = static_cast<int>(threadIdx.x) / W;
+    asm volatile("" : "+v"(y0));
+    return y0;
+  }
   __device__ __forceinline__ void set_layout(int kzb_) {
     kzb = kzb_;
     rs = static_cast<unsigned>(lines);
@@ -157,7 +165,7 @@ struct Stage {
       dsrc[S] = src;
       doff[S] = o;
     } else {
-      const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+      const int y0 = copy_row(), l = threadIdx.x % W;
       // rows >= N read row N-1 of the same (clamped) line
       const unsigned last = rowoff(N - 1) + lineoff(min(l0 + l, lines - 1));
 #pragma unroll
@@ -177,16 +185,18 @@ struct Stage {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's share of the copy landed
       lds_barrier();                                   // ... and every other wave's
       const T2* c = tile + w;
+      int ln = lane;  // (laundered: see copy_row)
+      asm volatile("" : "+v"(ln));
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int y = lane * R + r;
+        const int y = ln * R + r;
         const T2 v = c[(y < N ? y : 0) * W];  // raw image: rows >= N were never written
         x[0][r] = y < N ? static_cast<double>(v.x) : 0.0;
         x[1][r] = y < N ? static_cast<double>(v.y) : 0.0;
       }
       return;
     }
-    const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+    const int y0 = copy_row(), l = threadIdx.x % W;
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int y = y0 + RPB * q;
@@ -229,7 +239,7 @@ struct Stage {
       for (int r = 0; r < R; ++r) c[r * PITCH] = T2{static_cast<T>(sc * re[r]), static_cast<T>(sc * im[r])};
     }
     lds_barrier();
-    const int y0 = threadIdx.x / W, l = threadIdx.x % W;
+    const int y0 = copy_row(), l = threadIdx.x % W;
     if (line0 + l < lines) {
 #pragma unroll
       for (int q = 0; q < R; ++q) {

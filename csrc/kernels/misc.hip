@@ -122,7 +122,7 @@ void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp
 }
 
 void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool fp64, hipStream_t s) {
-  CH_CHECK(a.nblk >= 1 && a.nblk <= 8 && a.kx_start[0] == 0 && a.kx_start[a.nblk] == a.nkx,
+  CH_CHECK(a.nblk >= 1 && a.nblk <= kMaxSeg && a.kx_start[0] == 0 && a.kx_start[a.nblk] == a.nkx,
            "kz0 symmetrisation: bad kx block table");
   if (fp64)
     hipLaunchKernelGGL(kz0_sym_dist_kernel<double2>, dim3(a.N), dim3(128), 0, s, static_cast<double2*>(q),

@@ -141,14 +141,18 @@ def test_rccl_phase_timing(native):
     assert len(t) == 3 and all(x > 0 for x in t)
 
 
-@pytest.mark.parametrize("kblocks,self_mode", [("1", "direct"), ("2", "direct"), ("3", "direct"), ("8", "direct"),
-                                               ("4", "copy")])
-def test_rccl_kspec_blocks_overlap(native, monkeypatch, kblocks, self_mode):
-    """K-SPEC / exchange overlap: the spectral fields stored as kx sub-blocks,
-    K-SPEC run block by block and each block's backward exchange issued behind it on the comm
-    stream.  State, statistics, the kz = 0 symmetrisation and the spectra equal the fast path
+@pytest.mark.parametrize("kblocks,self_mode,fsplit", [("1", "direct", "1"), ("2", "direct", "1"), ("3", "direct", "1"),
+                                                      ("8", "direct", "1"), ("16", "direct", "1"), ("4", "copy", "1"),
+                                                      ("4", "direct", "0")])
+def test_rccl_kspec_blocks_overlap(native, monkeypatch, kblocks, self_mode, fsplit):
+    """K-SPEC / exchange overlap: the spectral fields stored as kx
+    sub-blocks, K-SPEC run block by block and each block's backward exchange issued behind it on
+    the comm stream; the last chunk's forward exchange returns block by block and K-SPEC block b
+    waits only for its own rows (fsplit = 1); 16 sub-blocks fill the 16 exchange segments of the
+    x transforms.  State, statistics, the kz = 0 symmetrisation and the spectra equal the fast path
     bitwise (the arithmetic per line and per tile is unchanged), eager and captured."""
     monkeypatch.setenv("CHANNEL_A2A_SELF", self_mode)
+    monkeypatch.setenv("CHANNEL_FWD_SPLIT", fsplit)
     monkeypatch.setenv("CHANNEL_YCHUNK", "7")
     res = []
     for uid, kb in ((b"", None), (native.new_unique_id(), kblocks)):
