@@ -39,7 +39,10 @@ constexpr int kspec_xmode() {
 // same as two (profiles/r03s3/ab_kspec_ns7.txt)
 template <int R, typename T>
 constexpr int kspec_slots() {
-  return R <= 4 ? 1 : (R <= 8 ? 2 : 1);
+  // fp64 R = 3 (Re_tau~180, 3.7k lines: two rounds of waves, latency-bound): two slots measured
+  // 0.470 ms/step at 128x129x128 against 0.475 / 0.502 with one (same box, run-to-run spread ~5 %;
+  // profiles/r04/ab_small_grid.txt); fp32 R = 3: no difference
+  return R <= 4 ? ((R == 3 && sizeof(T) == 8) ? 2 : 1) : (R <= 8 ? 2 : 1);
 }
 
 // dispatch a runtime R to the instantiated rows-per-lane values

@@ -1155,8 +1155,31 @@ static int kspec_ns7() {
   return ns;
 }
 
+// CHANNEL_KSPEC_VAR = w4 | ns2 (A/B at R = 3, the small grids): 4 lines per block instead of 8,
+// or two register prefetch slots instead of one
+static int kspec_var_env() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_VAR");
+    if (!e) return 0;
+    const std::string s(e);
+    return s == "w4" ? 1 : (s == "ns2" ? 2 : 0);
+  }();
+  return v;
+}
+
 template <int R, typename T, int PAR = 0>
 static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t stream) {
+  if constexpr (R == 3 && PAR == 0) {
+    if (const int v = kspec_var_env()) {
+      constexpr int W3 = 4;
+      auto k = v == 1 ? kspec_kernel<3, T, W3, 1, kspec_xmode<3, T>(), 0> : kspec_kernel<3, T, 8, 2, kspec_xmode<3, T>(), 0>;
+      const int w = v == 1 ? W3 : 8;
+      const int nt = (a.lines + w - 1) / w;
+      dim3 grid(std::min(nt, resident_blocks(reinterpret_cast<const void*>(k), w * 64))), block(w * 64);
+      hipLaunchKernelGGL(k, grid, block, 0, stream, t.tab, a);
+      return;
+    }
+  }
   if constexpr (R == 4 && sizeof(T) == 4) {
     if (t.H == 2) {
       // lines over two waves: 4 lines x 2 halves = 8 waves per workgroup (two per SIMD)
