@@ -257,20 +257,24 @@ std::vector<int> Config::spectra_plane_list() const {
   return out;
 }
 
-// transform lengths with kernels (kernels/fft.hip CH_DISPATCH_N): 2^k in [16, 2048], 3*2^k in
-// [48, 1536], 5*2^k in [80, 1280] (the reference's cuFFT plans take any length, fft.c:17-23)
+// transform lengths with kernels (kernels/fft.hip CH_DISPATCH_N): 2^k in [16, 2048], and m*2^k
+// (2^k >= 16, at most 2048 points) for m = 3, 5, 7, 9, 15 (the reference's cuFFT plans take any
+// length, fft.c:17-23)
 bool fft_length_supported(int n) {
   if (n < 16 || n > 2048) return false;
-  int m = n;
-  if (m % 3 == 0) m /= 3;
-  else if (m % 5 == 0) m /= 5;
-  return (m & (m - 1)) == 0 && m >= 16;
+  for (int m : {1, 3, 5, 7, 9, 15}) {
+    if (n % m) continue;
+    const int p = n / m;
+    if ((p & (p - 1)) == 0 && p >= 16) return true;
+  }
+  return false;
 }
+static const char* kFftLengths = "2^k (16..2048) or 3, 5, 7, 9, 15 times 2^k >= 16 (at most 2048)";
 
 void Config::validate() const {
-  CH_CHECK(fft_length_supported(NX), "NX=" << NX << " must be 2^k (16..2048), 3*2^k (48..1536) or 5*2^k (80..1280)");
+  CH_CHECK(fft_length_supported(NX), "NX=" << NX << " must be " << kFftLengths);
   CH_CHECK(NZ >= 9 && fft_length_supported(2 * NZ - 2),
-           "2*NZ-2=" << (2 * NZ - 2) << " (physical z points) must be 2^k (16..2048), 3*2^k (48..1536) or 5*2^k (80..1280)");
+           "2*NZ-2=" << (2 * NZ - 2) << " (physical z points) must be " << kFftLengths);
   CH_CHECK(NY >= 9 && NY <= 64 * 24, "NY=" << NY << " must be in [9, 1536]");
   CH_CHECK(Re > 0 && Q > 0 && LX > 0 && LZ > 0, "Re, Q, LX, LZ must be positive");
   CH_CHECK(stretch > 0, "stretch must be positive");

@@ -1,4 +1,4 @@
-// In-LDS batched complex FFT (Stockham autosort, mixed radix 16/12/10/8/6/5/4/3/2, radix 16 first).
+// In-LDS batched complex FFT (Stockham autosort, mixed radix 16/15/12/10/9/8/7/6/5/4/3/2, radix 16 first).
 //
 // All threads of the workgroup cooperate on ROWS rows of length N held in LDS.  Each pass gathers
 // its butterfly inputs into registers, synchronises, applies the inter-pass twiddles and an R-point
@@ -223,6 +223,62 @@ __device__ __forceinline__ void dft5(T2* v) {
 template <int R>
 struct RootTable;
 template <>
+struct RootTable<7> {
+  static constexpr double c[7] = {1.0, 0.62348980185873353053, -0.22252093395631440429, -0.90096886790241912624,
+                                  -0.90096886790241912624, -0.22252093395631440429, 0.62348980185873353053};
+  static constexpr double s[7] = {0.0, 0.78183148246802980871, 0.97492791218182360702, 0.43388373911755812048,
+                                  -0.43388373911755812048, -0.97492791218182360702, -0.78183148246802980871};
+};
+template <>
+struct RootTable<9> {
+  static constexpr double c[9] = {1.0, 0.76604444311897803520, 0.17364817766693034885, -0.5, -0.93969262078590838405,
+                                  -0.93969262078590838405, -0.5, 0.17364817766693034885, 0.76604444311897803520};
+  static constexpr double s[9] = {0.0, 0.64278760968653932632, 0.98480775301220805936, 0.86602540378443864676,
+                                  0.34202014332566873304, -0.34202014332566873304, -0.86602540378443864676,
+                                  -0.98480775301220805936, -0.64278760968653932632};
+};
+template <>
+struct RootTable<15> {
+  static constexpr double c[15] = {1.0, 0.91354545764260089550, 0.66913060635885821383, 0.30901699437494742410,
+                                   -0.10452846326765347140, -0.5, -0.80901699437494742410, -0.97814760073380563793,
+                                   -0.97814760073380563793, -0.80901699437494742410, -0.5, -0.10452846326765347140,
+                                   0.30901699437494742410, 0.66913060635885821383, 0.91354545764260089550};
+  static constexpr double s[15] = {0.0, 0.40673664307580020775, 0.74314482547739423501, 0.95105651629515357212,
+                                   0.99452189536827333692, 0.86602540378443864676, 0.58778525229247312917,
+                                   0.20791169081775933710, -0.20791169081775933710, -0.58778525229247312917,
+                                   -0.86602540378443864676, -0.99452189536827333692, -0.95105651629515357212,
+                                   -0.74314482547739423501, -0.40673664307580020775};
+};
+
+// radix 7 (forward sign; INV flips it): X_k = a_k - i b_k, X_{7-k} = a_k + i b_k with
+// a_k = v0 + sum_j cos(2 pi jk/7) (v_j + v_{7-j}), b_k = sum_j sin(2 pi jk/7) (v_j - v_{7-j})
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft7(T2* v) {
+  using T = decltype(v[0].x);
+  using RT = RootTable<7>;
+  T2 t[4], d[4];
+#pragma unroll
+  for (int j = 1; j <= 3; ++j) {
+    t[j] = cadd(v[j], v[7 - j]);
+    d[j] = csub(v[j], v[7 - j]);
+  }
+  const T2 v0 = v[0];
+  v[0] = cadd(v0, cadd(t[1], cadd(t[2], t[3])));
+#pragma unroll
+  for (int k = 1; k <= 3; ++k) {
+    T2 a = v0, b{T(0), T(0)};
+#pragma unroll
+    for (int j = 1; j <= 3; ++j) {
+      const T c = static_cast<T>(RT::c[(j * k) % 7]), sn = static_cast<T>(RT::s[(j * k) % 7]);
+      a = T2{a.x + c * t[j].x, a.y + c * t[j].y};
+      b = T2{b.x + sn * d[j].x, b.y + sn * d[j].y};
+    }
+    const T2 m = mul_mi<INV>(b);  // -i b (forward)
+    v[k] = cadd(a, m);
+    v[7 - k] = csub(a, m);
+  }
+}
+template <>
 struct RootTable<6> {
   static constexpr double c[6] = {1.0, 0.5, -0.5, -1.0, -0.5, 0.5};
   static constexpr double s[6] = {0.0, 0.86602540378443864676, 0.86602540378443864676, 0.0,
@@ -287,22 +343,26 @@ __device__ __forceinline__ void dftR(T2* v) {
   else if constexpr (R == 4) dft4<INV>(v);
   else if constexpr (R == 5) dft5<INV>(v);
   else if constexpr (R == 6) dft_ab<3, 2, INV>(v);
+  else if constexpr (R == 7) dft7<INV>(v);
   else if constexpr (R == 8) dft8<INV>(v);
+  else if constexpr (R == 9) dft_ab<3, 3, INV>(v);
   else if constexpr (R == 10) dft_ab<5, 2, INV>(v);
   else if constexpr (R == 12) dft_ab<4, 3, INV>(v);
+  else if constexpr (R == 15) dft_ab<5, 3, INV>(v);
   else {
     static_assert(R == 16, "unsupported radix");
     dft16<INV>(v);
   }
 }
 
-// radix plan: 16 first, then 16 or the rest, the odd factor (3 or 5, possibly inside a 6, 10 or
-// 12) in the last pass.  Host and device share this function (twiddle tables, kernels).
+// radix plan: 16 first, then 16 or the rest, the odd factor (3, 5, 7, 9 or 15, possibly inside a
+// 6, 10 or 12) in the last pass.  Host and device share this function (twiddle tables, kernels).
 struct Radices {
   int r0, r1, r2;
 };
 __host__ __device__ constexpr bool fft_radix_ok(int r) {
-  return r == 1 || r == 2 || r == 3 || r == 4 || r == 5 || r == 6 || r == 8 || r == 10 || r == 12 || r == 16;
+  return r == 1 || r == 2 || r == 3 || r == 4 || r == 5 || r == 6 || r == 7 || r == 8 || r == 9 || r == 10 ||
+         r == 12 || r == 15 || r == 16;
 }
 __host__ __device__ constexpr Radices fft_radices(int n) {
   if (n <= 16) return Radices{n, 1, 1};
@@ -312,6 +372,10 @@ __host__ __device__ constexpr Radices fft_radices(int n) {
   if (rem % 16 == 0 && fft_radix_ok(rem / 16)) return Radices{16, 16, rem / 16};
   const int odd = rem % 3 == 0 ? 3 : (rem % 5 == 0 ? 5 : 1);
   if (odd > 1 && fft_radix_ok(rem / odd)) return Radices{16, rem / odd, odd};
+  // 7 * 2^k, 9 * 2^k, 15 * 2^k: the whole odd factor in the last pass
+  const int odds[3] = {7, 9, 15};
+  for (int i = 0; i < 3; ++i)
+    if (rem % odds[i] == 0 && fft_radix_ok(rem / odds[i])) return Radices{16, rem / odds[i], odds[i]};
   return Radices{0, 0, 0};
 }
 __host__ __device__ constexpr bool fft_length_ok(int n) {

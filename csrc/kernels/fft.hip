@@ -39,7 +39,8 @@ void Twiddles::release() {
   buf = reg = nullptr;
 }
 
-// transform lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280)
+// transform lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280),
+// 7*2^k (112..1792), 9*2^k (144..1152), 15*2^k (240..1920)
 #define CH_CASE_N(V, ...) \
   case V: { constexpr int NN = V; __VA_ARGS__; } break;
 #define CH_DISPATCH_N(N_, ...)                                                                              \
@@ -51,6 +52,11 @@ void Twiddles::release() {
     CH_CASE_N(384, __VA_ARGS__) CH_CASE_N(768, __VA_ARGS__) CH_CASE_N(1536, __VA_ARGS__)                    \
     CH_CASE_N(80, __VA_ARGS__) CH_CASE_N(160, __VA_ARGS__) CH_CASE_N(320, __VA_ARGS__)                      \
     CH_CASE_N(640, __VA_ARGS__) CH_CASE_N(1280, __VA_ARGS__)                                                \
+    CH_CASE_N(112, __VA_ARGS__) CH_CASE_N(224, __VA_ARGS__) CH_CASE_N(448, __VA_ARGS__)                     \
+    CH_CASE_N(896, __VA_ARGS__) CH_CASE_N(1792, __VA_ARGS__)                                                \
+    CH_CASE_N(144, __VA_ARGS__) CH_CASE_N(288, __VA_ARGS__) CH_CASE_N(576, __VA_ARGS__)                     \
+    CH_CASE_N(1152, __VA_ARGS__) CH_CASE_N(240, __VA_ARGS__) CH_CASE_N(480, __VA_ARGS__)                    \
+    CH_CASE_N(960, __VA_ARGS__) CH_CASE_N(1920, __VA_ARGS__)                                                \
     default: CH_CHECK(false, "unsupported FFT length " << N_);                                              \
   }
 

@@ -541,11 +541,12 @@ constexpr int zphys_tpr(int esz = 4) {
   return esz == 4 ? (NZP >= 16 ? pow2_ceil((NZP + 15) / 16) : 1)
                   : (NZP >= 1024 ? 128 : (NZP >= 16 ? pow2_ceil((NZP + 7) / 8) : 1));
 }
-// rows per block: 2 at 2048 points (two row buffers + the twiddles fit twice per CU in fp32);
-// 4 waves' worth of rows below 64 threads per row
+// rows per block: 2 above 1536 points (two row buffers + the twiddles fit twice per CU in fp32;
+// four fp64 rows of 1792 points and their twiddles would exceed the LDS); 4 waves' worth of rows
+// below 64 threads per row
 template <int NZP, typename T, int TPR = zphys_tpr<NZP>(sizeof(T))>
 constexpr int zphys_rows() {
-  return TPR < 64 ? ZW * 64 / TPR : (NZP >= 2048 || (sizeof(T) == 4 && TPR == 128) ? 2 : ZW);
+  return TPR < 64 ? ZW * 64 / TPR : (NZP > 1536 || (sizeof(T) == 4 && TPR == 128) ? 2 : ZW);
 }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
@@ -1257,10 +1258,14 @@ void fft_test_len(void* data, int batch, int dir, const Twiddles& tw, bool fp64,
   }
 }
 
-// the lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280)
+// the lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280), 7*2^k (112..1792),
+// 9*2^k (144..1152), 15*2^k (240..1920)
 #define CH_FFT_POW2_LENGTHS(X) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048)
 #define CH_FFT_R3_LENGTHS(X) X(48) X(96) X(192) X(384) X(768) X(1536)
 #define CH_FFT_R5_LENGTHS(X) X(80) X(160) X(320) X(640) X(1280)
+#define CH_FFT_R7_LENGTHS(X) X(112) X(224) X(448) X(896) X(1792)
+#define CH_FFT_R9_LENGTHS(X) X(144) X(288) X(576) X(1152)
+#define CH_FFT_R15_LENGTHS(X) X(240) X(480) X(960) X(1920)
 #define CH_FFT_INSTANTIATE(NN)                                                                              \
   template void fft_xb_len<NN>(const XArgs&, const XSrc&, void*, const Twiddles&, bool, hipStream_t);      \
   template void fft_xf_len<NN>(const XArgs&, const void*, const XDst&, const Twiddles&, bool, hipStream_t); \
@@ -1275,5 +1280,8 @@ void fft_test_len(void* data, int batch, int dir, const Twiddles& tw, bool fp64,
 CH_FFT_POW2_LENGTHS(CH_FFT_EXTERN_ALL)
 CH_FFT_R3_LENGTHS(CH_FFT_EXTERN_ALL)
 CH_FFT_R5_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R7_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R9_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R15_LENGTHS(CH_FFT_EXTERN_ALL)
 
 }  // namespace channel

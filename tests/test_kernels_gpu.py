@@ -81,10 +81,11 @@ def test_d1_dense_mfma(native, NY):
 
 
 @pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048,
-                               48, 96, 192, 384, 768, 1536, 80, 160, 320, 640, 1280])
+                               48, 96, 192, 384, 768, 1536, 80, 160, 320, 640, 1280,
+                               112, 224, 448, 896, 1792, 144, 288, 576, 1152, 240, 480, 960, 1920])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_fft_c2c(native, n, dtype):
-    """Batched C2C against numpy, powers of two and the radix-3 / radix-5 plans (3*2^k, 5*2^k)."""
+    """Batched C2C against numpy, powers of two and the radix-3/5/7/9/15 plans (m*2^k)."""
     rng = np.random.default_rng(n)
     x = rng.standard_normal((7, n)) + 1j * rng.standard_normal((7, n))
     xt = torch.tensor(x, dtype=dtype, device=DEV)
@@ -96,7 +97,9 @@ def test_fft_c2c(native, n, dtype):
 
 
 @pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20), (2048, 9),
-                                    (96, 13), (192, 11), (384, 20), (768, 9), (1536, 5), (80, 7), (1280, 6)])
+                                    (96, 13), (192, 11), (384, 20), (768, 9), (1536, 5), (80, 7), (1280, 6),
+                                    (112, 9), (448, 13), (1792, 5), (144, 7), (1152, 6), (240, 11), (960, 7),
+                                    (1920, 5)])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_xfft(native, NX, nkz, dtype):
     rng = np.random.default_rng(NX)
@@ -125,6 +128,11 @@ def test_xfft(native, NX, nkz, dtype):
                                           (4, 768, torch.complex128), (2, 1536, torch.complex64),
                                           (4, 1536, torch.complex128), (4, 1280, torch.complex64),
                                           (8, 160, torch.complex128),
+                                          (8, 112, torch.complex128), (4, 448, torch.complex64),
+                                          (2, 1792, torch.complex64), (2, 1792, torch.complex128),
+                                          (8, 144, torch.complex64), (4, 1152, torch.complex128),
+                                          (8, 240, torch.complex128), (4, 960, torch.complex64),
+                                          (2, 1920, torch.complex64), (2, 1920, torch.complex128),
                                           (1024, 1024, torch.complex64), (1024, 1024, torch.complex128),
                                           (512, 2048, torch.complex64)])
 def test_zphys(native, NX, Nzp, dtype):
