@@ -734,6 +734,8 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
     // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
     const int yl = rv ? static_cast<int>(r / a.NX) : 0;
     const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    // (the CFL sum in fp32: a double kx_max promoted every point's sum to fp64, 2 cvt + 2 FMA64 per point)
+    const float cxf = static_cast<float>(a.cx), czf = static_cast<float>(a.cz);
     T hz[EP];
     T2 hxy[kRegEdge ? EP : 1];
 #pragma unroll
@@ -745,7 +747,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       mu = fmaxf(mu, au);
       mv = fmaxf(mv, av);
       mw = fmaxf(mw, aw);
-      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+      mc = fmaxf(mc, au * cxf + av * idy + aw * czf);
       const int n = t + TPR * i;
       if constexpr (kRegEdge) hxy[i] = T2{hx, hy};
       else if (n < NZP) row[fft_pidx(n)] = T2{hx, hy};
@@ -1067,6 +1069,8 @@ __global__ void __launch_bounds__(256) zphys_reg_kernel(ZArgs a, typename C2<T>:
     // rotational product H = u x omega (convolution_kernels.cu:125-131) and CFL maxima
     const int yl = static_cast<int>(r / a.NX);
     const float idy = static_cast<float>(a.inv_dy[a.y0 + yl]);
+    // (the CFL sum in fp32: a double kx_max promoted every point's sum to fp64, 2 cvt + 2 FMA64 per point)
+    const float cxf = static_cast<float>(a.cx), czf = static_cast<float>(a.cz);
     T2 hxy[M], hz[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -1077,7 +1081,7 @@ __global__ void __launch_bounds__(256) zphys_reg_kernel(ZArgs a, typename C2<T>:
       mu = fmaxf(mu, au);
       mv = fmaxf(mv, av);
       mw = fmaxf(mw, aw);
-      mc = fmaxf(mc, static_cast<float>(au * a.cx + av * idy + aw * a.cz));
+      mc = fmaxf(mc, au * cxf + av * idy + aw * czf);
     }
     if (!(a.diag & 1)) {
       reg_fft_fwd<M>(hxy, buf, tw1, tw64, lane);

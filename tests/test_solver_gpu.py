@@ -179,6 +179,17 @@ def test_t_end_stops_run(native):
     assert s2.steps_done() == 41 and abs(s2.time() - 0.41) < 1e-12
 
 
+def test_t_end_with_cfl_dt_at_dt_max(native):
+    """Variable dt (no dt_fixed): a laminar start whose CFL step exceeds dt_max runs at dt_max from the
+    first step; the host-side t_end decision uses dt_max as its margin (a multiple of the
+    previous dt is no bound), so the run still stops at the first step that reaches t_end."""
+    s = make_solver(native, NX=32, NY=33, NZ=17, Re=400.0, precision="fp64", ic="laminar", stats_every=0,
+                    log_every=0, symmetry_every=0, dt_max=0.01, t_end=0.035)
+    s.init_ic()
+    s.run(100, False)
+    assert s.steps_done() == 4 and abs(s.time() - 0.04) < 1e-12
+
+
 def test_phase_times_add_up(native):
     """Per-phase event timing (serialised chunked pipeline) accounts for the whole step."""
     s = make_solver(native, NX=512, NY=257, NZ=257, Re=11150.0, precision="fp32", ic="random", stats_every=0,
