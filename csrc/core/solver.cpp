@@ -174,9 +174,11 @@ Solver::~Solver() {
 
 void Solver::alloc() {
   const Plan& p = plan_;
-  // blocked spectral layout at one rank (CHANNEL_SPEC_KZB=0: the plain [y][line] layout, A/B);
-  // P > 1 keeps [y][line]: its exchange blocks are row ranges of every line
-  kzb_ = comm_ ? 0 : kSpecKzBlock;
+  // blocked spectral layout at one rank (CHANNEL_SPEC_KZB=0/1 forces it off/on, A/B); P > 1 keeps
+  // [y][line]: its exchange blocks are row ranges of every line.  Default on where it measured
+  // faster: R = 7, 8 (1024x385x1024: 39.5 -> 35.8 ms/step); the plain layout stays at R = 5
+  // (512x257x512: 7.37 vs 7.63) and R = 10 (2048x633x2048: 315 vs 323; profiles/r04/ab_layout_grids.txt)
+  kzb_ = (!comm_ && p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();
