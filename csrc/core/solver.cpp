@@ -179,6 +179,10 @@ void Solver::alloc() {
   // faster: R = 7, 8 (1024x385x1024: 39.5 -> 35.8 ms/step); the plain layout stays at R = 5
   // (512x257x512: 7.37 vs 7.63) and R = 10 (2048x633x2048: 315 vs 323; profiles/r04/ab_layout_grids.txt)
   kzb_ = (!comm_ && p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
+  // (the x transforms address a blocked field with 32-bit byte offsets)
+  if (kzb_ && static_cast<unsigned long long>(spec_rows(kSpecKzBlock, p.NY)) * p.nkx_loc *
+                      ((p.nkz_loc + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock) * (fp64_ ? 16 : 8) >= (1ull << 32))
+    kzb_ = 0;
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();

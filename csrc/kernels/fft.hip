@@ -82,6 +82,13 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   CH_CHECK(a.Kx == a.NX / 3 && a.nkx == 2 * a.Kx + 1, "xfft_backward: retained kx must be the 2/3 rule's (Kx = NX/3)");
   CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_backward: per-field plane block exceeds 32-bit offsets");
+  // one-source / blocked-layout paths address with 32-bit BYTE offsets (fft_impl.hpp at_byte)
+  const long long esz = fp64 ? 16 : 8;
+  CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz * esz < (1LL << 32),
+           "xfft_backward: a field's x-expanded chunk exceeds 4 GiB (use smaller y chunks)");
+  CH_CHECK(!a.kzb || a.field_stride_spec * esz < (1LL << 32), "xfft_backward: blocked spectral field exceeds 4 GiB");
+  CH_CHECK(src.nsrc > 1 || src.self_seg >= 0 || static_cast<long long>(a.ny) * a.nkx * a.nkz * esz < (1LL << 32),
+           "xfft_backward: a field's spectral chunk exceeds 4 GiB (use smaller y chunks)");
   CH_DISPATCH_N(a.NX, fft_xb_len<NN>(a, src, phys, tw, fp64, s));
   HIP_LAUNCH_CHECK(s);
 }
@@ -91,6 +98,12 @@ void xfft_forward(const XArgs& a_in, const void* phys, const XDst& dst, const Tw
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_forward: twiddle table mismatch");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_forward: per-field plane block exceeds 32-bit offsets");
   CH_CHECK(static_cast<long long>(a.ny) * a.nkx * a.nkz < (1LL << 32), "xfft_forward: per-field spectral block exceeds 32-bit offsets");
+  const long long esz = fp64 ? 16 : 8;
+  CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz * esz < (1LL << 32),
+           "xfft_forward: a field's x-expanded chunk exceeds 4 GiB (use smaller y chunks)");
+  CH_CHECK(!a.kzb || a.field_stride_spec * esz < (1LL << 32), "xfft_forward: blocked spectral field exceeds 4 GiB");
+  CH_CHECK(dst.ndst > 1 || dst.self_seg >= 0 || static_cast<long long>(a.ny) * a.nkx * a.nkz * esz < (1LL << 32),
+           "xfft_forward: a field's spectral chunk exceeds 4 GiB (use smaller y chunks)");
   CH_DISPATCH_N(a.NX, fft_xf_len<NN>(a, phys, dst, tw, fp64, s));
   HIP_LAUNCH_CHECK(s);
 }

@@ -143,6 +143,17 @@ template <typename T2, int V>
 struct alignas(sizeof(T2) * V) CVec {
   T2 c[V];
 };
+// element at a 32-bit BYTE offset from a wave-uniform base: the global access then takes the base
+// in SGPRs and the offset in one VGPR (saddr form) instead of 64-bit address arithmetic per
+// element; every caller's span is checked below 4 GiB on the host
+template <typename P>
+__device__ __forceinline__ P& at_byte(P* base, unsigned off) {
+  return *reinterpret_cast<P*>(reinterpret_cast<char*>(base) + off);
+}
+template <typename P>
+__device__ __forceinline__ const P& at_byte(const P* base, unsigned off) {
+  return *reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + off);
+}
 
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
 // LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
@@ -211,13 +222,15 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       static_assert(NT % CW == 0, "a thread's column must be the same for every access");
       constexpr int DI = NT / CW;
       const int c = (tid % CW) * V;
-      const T2* bt = base + spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V));
-      const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock;
+      const unsigned bt = spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V)) *
+                          static_cast<unsigned>(sizeof(T2));
+      const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
+      const CV* bv = reinterpret_cast<const CV*>(base);
 #pragma unroll
       for (int q = 0; q < EPT; ++q) {
         int i = tid / CW + q * DI;
         if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
-        v[q] = *reinterpret_cast<const CV*>(bt + static_cast<unsigned>(i) * rs);
+        v[q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
       }
       return;
     }
@@ -232,8 +245,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int c = (e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V);
       if constexpr (SM == kSegOne) {
-        v[q] = *reinterpret_cast<const CV*>(
-            base + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz));
+        v[q] = at_byte(reinterpret_cast<const CV*>(base),
+                       (static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
+                           static_cast<unsigned>(sizeof(T2)));
       } else {
         const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                         : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
@@ -303,8 +317,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
           *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
         } else {
-          *reinterpret_cast<CV*>(out + static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
-                                 static_cast<unsigned>(kz)) = w;
+          at_byte(reinterpret_cast<CV*>(out), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
+                                               static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
         }
       }
     }
@@ -366,8 +380,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
                                             static_cast<unsigned>(yy * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) +
                                             static_cast<unsigned>(kz));
       } else {
-        v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
-                                            static_cast<unsigned>(kz));
+        v[q] = at_byte(reinterpret_cast<const CV*>(in), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
+                                                         static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
       }
     }
   };
@@ -407,14 +421,15 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int c = (tid % CW) * V;
       const int kz = kz0 + c % KC, yy = y + c / KC;
       if (kz < a.nkz && yy < a.ny) {
-        T2* ot = outb + spec_blk_off(a, yy, 0, kz);
-        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock;
+        const unsigned ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
+        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
+        CV* ov = reinterpret_cast<CV*>(outb);
         for (int i = tid / CW; i < a.nkx; i += NT / CW) {
           const int x = i <= a.Kx ? i : NX - (a.nkx - i);
           CV w;
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          *reinterpret_cast<CV*>(ot + static_cast<unsigned>(i) * rs) = w;
+          at_byte(ov, ot + static_cast<unsigned>(i) * rs) = w;
         }
       }
       continue;
@@ -431,8 +446,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SM == kSegOne) {
-          *reinterpret_cast<CV*>(outb + static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
-                                 static_cast<unsigned>(kz)) = w;
+          at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
+                                                static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
         } else {
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
                                           : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
@@ -587,13 +602,15 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   const int Kz = a.nkz - 1, nkz = a.nkz;
   const long long fs = a.field_stride;
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
-  // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz)
+  // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz, 32-bit:
+  // one segment runs only when a field's rows fit 4 GiB (zphys_launch_tpr), so a field's accesses
+  // are a uniform 64-bit base plus a 32-bit lane byte offset -- no 64-bit arithmetic per element)
   auto zaddr = [&](long long r, int k) -> long long {
     if constexpr (SEG) {
       const SegPos sp = seg_find(a.kz_start, a.off, a.nseg, k);
       return sp.off + r * sp.count + (k - sp.start);
     } else {
-      return r * nkz + k;
+      return static_cast<long long>(static_cast<unsigned>(r) * static_cast<unsigned>(nkz) + static_cast<unsigned>(k));
     }
   };
   // retained kz per thread: nkz = Nzp/3 + 1 (2/3 rule; checked on the host)
@@ -602,13 +619,38 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
     const bool rv = TPR < 64 ? r < nrows : true;
     const T2* A = fields + (2 * p) * fs;
     const T2* B = fields + (2 * p + 1) * fs;
+    if constexpr (!SEG) {
+      // unconditional loads at a clamped (in-bounds) index, zeros selected afterwards: a guarded
+      // load is a branch, an exec-mask save/restore and a zero move per element
+      const unsigned rb = static_cast<unsigned>(rv ? r : nrows - 1) * static_cast<unsigned>(nkz);
 #pragma unroll
-    for (int i = 0; i < MK; ++i) {
-      const int k = t + TPR * i;
-      const bool ld = k < nkz && rv;
-      const long long o = ld ? zaddr(r, k) : 0;
-      va[i] = ld ? A[o] : T2{0, 0};
-      vb[i] = ld ? B[o] : T2{0, 0};
+      for (int i = 0; i < MK; ++i) {
+        const int k = t + TPR * i;
+        const bool ld = k < nkz && rv;
+        const unsigned o = (rb + static_cast<unsigned>(min(k, nkz - 1))) * static_cast<unsigned>(sizeof(T2));
+        const T2 x = *reinterpret_cast<const T2*>(reinterpret_cast<const char*>(A) + o);
+        const T2 y = *reinterpret_cast<const T2*>(reinterpret_cast<const char*>(B) + o);
+        va[i] = ld ? x : T2{0, 0};
+        vb[i] = ld ? y : T2{0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MK; ++i) {
+        const int k = t + TPR * i;
+        const bool ld = k < nkz && rv;
+        const long long o = ld ? zaddr(r, k) : 0;
+        va[i] = ld ? A[o] : T2{0, 0};
+        vb[i] = ld ? B[o] : T2{0, 0};
+      }
+    }
+  };
+  // store of field f at element offset o (one segment: a 32-bit byte offset from the field base)
+  auto zstore = [&](int f, long long o, T2 v) {
+    if constexpr (!SEG) {
+      *reinterpret_cast<T2*>(reinterpret_cast<char*>(fields + f * fs) +
+                             static_cast<unsigned>(o) * static_cast<unsigned>(sizeof(T2))) = v;
+    } else {
+      fields[f * fs + o] = v;
     }
   };
   // The next pair's loads are in flight during each transform where the registers fit (fp32,
@@ -778,8 +820,8 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
         if (k < nkz) {
           const T2 Z = z[i];
           const long long o = zaddr(r, k);
-          fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
-          fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+          zstore(0, o, T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc});
+          zstore(1, o, T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc});
         }
       }
     } else {
@@ -801,8 +843,8 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
         if (k < nkz && rv) {
           const T2 Z = z0[i], Zm = z1[i];
           const long long o = zaddr(r, k);
-          fields[0 * fs + o] = T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc};
-          fields[1 * fs + o] = T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc};
+          zstore(0, o, T2{(Z.x + Zm.x) * sc, (Z.y - Zm.y) * sc});
+          zstore(1, o, T2{(Z.y + Zm.y) * sc, -(Z.x - Zm.x) * sc});
         }
       }
     }
@@ -843,7 +885,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           const T2 E2{z0[i].x + z1[i].x, z0[i].y - z1[i].y};
           const T2 O2{z0[i].y + z1[i].y, z1[i].x - z0[i].x};
           const T2 X = cadd(E2, cmul_tw<false>(O2, wk[i]));
-          fields[2 * fs + zaddr(r, k)] = T2{X.x * sc, X.y * sc};
+          zstore(2, zaddr(r, k), T2{X.x * sc, X.y * sc});
         }
       }
     } else {
@@ -867,7 +909,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
-        if (k < nkz && rv) fields[2 * fs + zaddr(r, k)] = T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc};
+        if (k < nkz && rv) zstore(2, zaddr(r, k), T2{(z0[i].x + z1[i].x) * sc, (z0[i].y - z1[i].y) * sc});
       }
     }
     }
@@ -1161,8 +1203,10 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
   using T2 = typename C2<T>::type;
   constexpr int ZR = zphys_rows<NN, T, TPR>();
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
-  auto kern = a.nseg > 1 ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
-                         : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
+  // (one segment with 32-bit byte offsets when a field's rows fit 4 GiB; the segment path otherwise)
+  const bool seg = a.nseg > 1 || static_cast<unsigned long long>(nrows) * a.nkz * sizeof(T2) >= (1ull << 32);
+  auto kern = seg ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
+                  : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
   const long long ngroups = (nrows + ZR - 1) / ZR;
   const long long cap = zpers_enabled() ? persist_blocks(reinterpret_cast<const void*>(kern), ZR * TPR, "CHANNEL_Z_BPC") : ngroups;
   dim3 grid(static_cast<unsigned>(std::min(ngroups, cap)));
