@@ -79,7 +79,7 @@ __host__ __device__ inline size_t spec_index(int kzb, int nkx, int nkzs, int y, 
   return spec_row_off(kzb, nkx * nkzs, y) + spec_line_off(kzb, ikx * nkzs + kz);
 }
 // rows allocated per spectral field (kzb: whole 8-plane chunks)
-inline int spec_rows(int kzb, int N) { return kzb ? (N + kSpecYBlock - 1) / kSpecYBlock * kSpecYBlock : N; }
+__host__ __device__ inline int spec_rows(int kzb, int N) { return kzb ? (N + kSpecYBlock - 1) / kSpecYBlock * kSpecYBlock : N; }
 
 // ---- the fused spectral (y-line) substep kernel ---------------------------------------------
 struct SpecArgs {
