@@ -96,6 +96,7 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
 void xfft_forward(const XArgs& a_in, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s) {
   const XArgs a = norm_pseg(a_in);
   CH_CHECK(tw.n == a.NX && tw.fp64 == fp64, "xfft_forward: twiddle table mismatch");
+  CH_CHECK(a.Kx == a.NX / 3 && a.nkx == 2 * a.Kx + 1, "xfft_forward: retained kx must be the 2/3 rule's (Kx = NX/3)");
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_forward: per-field plane block exceeds 32-bit offsets");
   CH_CHECK(static_cast<long long>(a.ny) * a.nkx * a.nkz < (1LL << 32), "xfft_forward: per-field spectral block exceeds 32-bit offsets");
   const long long esz = fp64 ? 16 : 8;

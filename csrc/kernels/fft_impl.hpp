@@ -177,6 +177,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   constexpr int CW = C / V;  // accesses per tile row (V kz columns each; the host checks nkz % V == 0)
   // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
   constexpr int NKMAX = 2 * (NX / 3) + 1;
+  constexpr int NKX = NKMAX, KXH = NX / 3;  // retained kx: the 2/3 rule's (checked on the host)
   constexpr int EPT = (NKMAX * CW + NT - 1) / NT;
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
@@ -194,7 +195,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int ntiles = nyt * nkzc * a.nfields;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
-  const int nload = a.nkx * CW;
+  const int nload = NKX * CW;
   CV v[EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
   // tile t -> (f, y0, kz0); at each iteration the blocks of one XCD take consecutive tiles
@@ -241,12 +242,12 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int e = tid + q * NT;
       // unconditional load from a clamped valid address: rows i >= nkx are never staged,
       // columns kz >= nkz are transformed (independently) but never stored
-      const int i = min(e / CW, a.nkx - 1);
+      const int i = min(e / CW, NKX - 1);
       const int c = (e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V);
       if constexpr (SM == kSegOne) {
         v[q] = at_byte(reinterpret_cast<const CV*>(base),
-                       (static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
+                       (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
                            static_cast<unsigned>(sizeof(T2)));
       } else {
         const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
       const int i = e / CW, c = (e - i * CW) * V;
-      const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+      const int x = i <= KXH ? i : NX - (NKX - i);
       if (e < nload)
 #pragma unroll
         for (int u = 0; u < V; ++u)
@@ -334,6 +335,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
   constexpr int CW = C / V;
   constexpr int EPT = (NX * CW + NT - 1) / NT;
+  constexpr int NKX = 2 * (NX / 3) + 1, KXH = NX / 3;  // retained kx: the 2/3 rule's (checked on the host)
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
@@ -424,8 +426,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         const unsigned ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
         const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
         CV* ov = reinterpret_cast<CV*>(outb);
-        for (int i = tid / CW; i < a.nkx; i += NT / CW) {
-          const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+        for (int i = tid / CW; i < NKX; i += NT / CW) {
+          const int x = i <= KXH ? i : NX - (NKX - i);
           CV w;
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
@@ -436,17 +438,17 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     // this rank's own block goes straight into its spectral field (no self exchange)
     T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
-    for (int e0 = 0; e0 < a.nkx * CW; e0 += NT) {
+    for (int e0 = 0; e0 < NKX * CW; e0 += NT) {
       const int e = e0 + tid;
       const int i = e / CW, c = (e - i * CW) * V;
       const int kz = kz0 + c % KC, yy = y + c / KC;
-      if (e < a.nkx * CW && kz < a.nkz && yy < a.ny) {
-        const int x = i <= a.Kx ? i : NX - (a.nkx - i);
+      if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
+        const int x = i <= KXH ? i : NX - (NKX - i);
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SM == kSegOne) {
-          at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * a.nkx + i) * static_cast<unsigned>(a.nkz) +
+          at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) +
                                                 static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
         } else {
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
@@ -599,7 +601,9 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   int ft = tid % TPRF;
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   const long long ngroups = (nrows + ZWT - 1) / ZWT;
-  const int Kz = a.nkz - 1, nkz = a.nkz;
+  // one segment holds every retained kz (Nzp/3 + 1: the launcher checks it), a compile-time count,
+  // so only the last of a thread's kz slots needs a bound check
+  const int nkz = SEG ? a.nkz : NZP / 3 + 1, Kz = nkz - 1;
   const long long fs = a.field_stride;
   float mu = 0.f, mv = 0.f, mw = 0.f, mc = 0.f;
   // element offset of (row r, kz) in the kz-blocked row layout (one block: r * nkz + kz, 32-bit:
@@ -1204,7 +1208,8 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
   constexpr int ZR = zphys_rows<NN, T, TPR>();
   const long long nrows = static_cast<long long>(a.ny) * a.NX;
   // (one segment with 32-bit byte offsets when a field's rows fit 4 GiB; the segment path otherwise)
-  const bool seg = a.nseg > 1 || static_cast<unsigned long long>(nrows) * a.nkz * sizeof(T2) >= (1ull << 32);
+  const bool seg = a.nseg > 1 || a.nkz != NN / 3 + 1 ||
+                   static_cast<unsigned long long>(nrows) * a.nkz * sizeof(T2) >= (1ull << 32);
   auto kern = seg ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
                   : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
   const long long ngroups = (nrows + ZR - 1) / ZR;
