@@ -737,6 +737,13 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.zero_mean_field = 4;  // omega_y's spectral source is the omega state (mean line = U)
   xa.kz_glob0 = p.kz0;
   xa.lds_poison = lds_poison_enabled() ? 1 : 0;
+  {
+    static const int xnt = [] {
+      const char* e = std::getenv("CHANNEL_XNT");
+      return e ? std::atoi(e) : 1;
+    }();
+    xa.nt = xnt;
+  }
   ZArgs za;
   za.lds_poison = xa.lds_poison;
   za.NX = p.NX;

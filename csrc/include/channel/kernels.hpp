@@ -180,6 +180,8 @@ struct XArgs {
   // blocked spectral layout (one rank, one source block; spec_index with kzb = 8): rows spec_y0 ..
   // spec_y0 + ny - 1 of fields of line stride nkzs (lines = nkx * nkzs)
   int kzb = 0, nkzs = 0, spec_y0 = 0;
+  int nt = 0;                        // streaming (non-temporal) spectral accesses (solver default 1;
+                                     // CHANNEL_XNT=0 off: 35.0 vs 34.75 ms/step, profiles/r04/ab_xnt.txt)
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);

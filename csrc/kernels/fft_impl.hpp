@@ -154,6 +154,39 @@ template <typename P>
 __device__ __forceinline__ const P& at_byte(const P* base, unsigned off) {
   return *reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + off);
 }
+// streaming (non-temporal) access of the spectral fields, which the x kernels read or write once
+// per substep (XArgs::nt): they then do not displace the x-expanded intermediates of the chunks in
+// flight from the Infinity Cache
+template <typename P>
+__device__ __forceinline__ P ld_nt(const P& r) {
+  static_assert(sizeof(P) == 8 || sizeof(P) == 16, "8- or 16-byte accesses");
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  P out;
+  if constexpr (sizeof(P) == 16) {
+    const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(&r));
+    __builtin_memcpy(&out, &x, 16);
+  } else {
+    const v2u x = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(&r));
+    __builtin_memcpy(&out, &x, 8);
+  }
+  return out;
+}
+template <typename P>
+__device__ __forceinline__ void st_nt(P& r, const P& v) {
+  static_assert(sizeof(P) == 8 || sizeof(P) == 16, "8- or 16-byte accesses");
+  typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  if constexpr (sizeof(P) == 16) {
+    v4u x;
+    __builtin_memcpy(&x, &v, 16);
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(&r));
+  } else {
+    v2u x;
+    __builtin_memcpy(&x, &v, 8);
+    __builtin_nontemporal_store(x, reinterpret_cast<v2u*>(&r));
+  }
+}
 
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
 // LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
@@ -227,11 +260,20 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
                           static_cast<unsigned>(sizeof(T2));
       const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
       const CV* bv = reinterpret_cast<const CV*>(base);
+      if (a.nt) {
 #pragma unroll
-      for (int q = 0; q < EPT; ++q) {
-        int i = tid / CW + q * DI;
-        if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
-        v[q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
+        for (int q = 0; q < EPT; ++q) {
+          int i = tid / CW + q * DI;
+          if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
+          v[q] = ld_nt(at_byte(bv, bt + static_cast<unsigned>(i) * rs));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < EPT; ++q) {
+          int i = tid / CW + q * DI;
+          if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
+          v[q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
+        }
       }
       return;
     }
@@ -246,9 +288,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int c = (e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V);
       if constexpr (SM == kSegOne) {
-        v[q] = at_byte(reinterpret_cast<const CV*>(base),
-                       (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
-                           static_cast<unsigned>(sizeof(T2)));
+        const CV& r = at_byte(reinterpret_cast<const CV*>(base),
+                              (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
+                                  static_cast<unsigned>(sizeof(T2)));
+        v[q] = a.nt ? ld_nt(r) : r;
       } else {
         const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                         : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
@@ -431,7 +474,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           CV w;
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          at_byte(ov, ot + static_cast<unsigned>(i) * rs) = w;
+          if (a.nt) st_nt(at_byte(ov, ot + static_cast<unsigned>(i) * rs), w);
+          else at_byte(ov, ot + static_cast<unsigned>(i) * rs) = w;
         }
       }
       continue;
@@ -448,8 +492,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
         if constexpr (SM == kSegOne) {
-          at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) +
-                                                static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
+          CV& r = at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) +
+                                                        static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
+          if (a.nt) st_nt(r, w);
+          else r = w;
         } else {
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
                                           : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
