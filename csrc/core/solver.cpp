@@ -738,11 +738,13 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.kz_glob0 = p.kz0;
   xa.lds_poison = lds_poison_enabled() ? 1 : 0;
   {
+    // streaming spectral accesses only where the spectral fields cannot stay in the 256 MB
+    // Infinity Cache anyway (a small grid's fields, written by K-SPEC, are read back from it)
     static const int xnt = [] {
       const char* e = std::getenv("CHANNEL_XNT");
-      return e ? std::atoi(e) : 1;
+      return e ? std::atoi(e) : -1;
     }();
-    xa.nt = xnt;
+    xa.nt = xnt >= 0 ? xnt : (6ull * spec_ * esz_ > (256ull << 20) ? 1 : 0);
   }
   ZArgs za;
   za.lds_poison = xa.lds_poison;
