@@ -187,6 +187,11 @@ void Solver::alloc() {
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();
   spec_ = static_cast<size_t>(spec_rows(kzb_, p.NY)) * p.nkx_loc * nkzs_;
+  // streaming (non-temporal) spectral accesses in the x transforms only where the spectral fields
+  // cannot stay in the 256 MB Infinity Cache anyway (a small grid's fields, written by K-SPEC, are
+  // read back from it); CHANNEL_XNT=0/1 forces it (read per Solver)
+  xnt_ = 6ull * spec_ * esz_ > (256ull << 20) ? 1 : 0;
+  if (const char* e = std::getenv("CHANNEL_XNT")) xnt_ = std::atoi(e) != 0 ? 1 : 0;
   physn_ = p.phys_elems();
   // kx sub-blocks (K-SPEC / exchange overlap): slab with a communicator only; the same count on
   // every rank (a function of Pc and the environment), at most kMaxSeg exchange segments in total
@@ -737,15 +742,7 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.zero_mean_field = 4;  // omega_y's spectral source is the omega state (mean line = U)
   xa.kz_glob0 = p.kz0;
   xa.lds_poison = lds_poison_enabled() ? 1 : 0;
-  {
-    // streaming spectral accesses only where the spectral fields cannot stay in the 256 MB
-    // Infinity Cache anyway (a small grid's fields, written by K-SPEC, are read back from it)
-    static const int xnt = [] {
-      const char* e = std::getenv("CHANNEL_XNT");
-      return e ? std::atoi(e) : -1;
-    }();
-    xa.nt = xnt >= 0 ? xnt : (6ull * spec_ * esz_ > (256ull << 20) ? 1 : 0);
-  }
+  xa.nt = xnt_;
   ZArgs za;
   za.lds_poison = xa.lds_poison;
   za.NX = p.NX;

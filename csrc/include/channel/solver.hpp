@@ -251,6 +251,7 @@ class Solver {
   // inside its graph) or, after anything that recomputed the outputs (prepare()), eagerly before
   // the step.  presend_done_: that exchange has been issued for the next substep 0.
   bool presend_done_ = false;
+  int xnt_ = 0;  // non-temporal spectral accesses in the x transforms (XArgs::nt)
   bool kb_overlap() const { return nkb_ > 1 && comm_ != nullptr; }
   // Forward-path overlap (slab, kx sub-blocks): the last y chunk's forward exchange goes out block
   // by block (ev_fb_[b] on the comm stream) and K-SPEC block b waits only for block b's rows.

@@ -426,3 +426,25 @@ def test_lds_poison_mode_is_bitwise(native, precision, NX, NY, NZ):
         assert np.all(np.isfinite(b[f]))
         assert np.array_equal(a[f], b[f]), f"field {f}"
     assert np.allclose(sa, sb, rtol=1e-12, atol=0)  # (plane sums: atomic order may differ)
+
+
+@pytest.mark.parametrize("NX,NY,NZ,precision", [(64, 385, 33, "fp32"), (96, 129, 49, "fp64")])
+def test_nontemporal_spectral_access_is_bitwise(native, monkeypatch, NX, NY, NZ, precision):
+    """Non-temporal spectral reads (x-backward) and writes (x-forward), on by default only for grids
+    whose spectral fields exceed the Infinity Cache: forced on for small grids (the tiled layout at
+    NY = 385, the plain one at 129), the run equals the cached-access run bitwise."""
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=2000.0, precision=precision, ic="random", ic_amplitude=0.05,
+              stats_every=0, log_every=0, symmetry_every=0, dt_fixed=2e-4)
+    res = []
+    for nt in ("0", "1"):
+        monkeypatch.setenv("CHANNEL_XNT", nt)
+        s = make_solver(native, **kw)
+        s.init_ic()
+        s.prepare()
+        for _ in range(3):
+            s.step(False)
+        assert s.health() == 0
+        res.append(s.get_state())
+        del s
+    for f in range(3):
+        assert np.array_equal(res[0][f], res[1][f]), f"field {f}"
