@@ -189,6 +189,7 @@ PYBIND11_MODULE(_core, m) {
       .def("log", &Solver::log, py::call_guard<py::gil_scoped_release>())
       .def("stats", [](Solver& s) { return vec(s.stats()); })
       .def("kblocks", &Solver::kblocks)
+      .def("bwd_blocks_issued", &Solver::bwd_blocks_issued)
       .def("mean_profile", [](Solver& s) { return vec(s.mean_profile()); })
       .def("health", &Solver::health)
       .def("time", &Solver::time)

@@ -84,7 +84,12 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
     sa.sin_addr.s_addr = htonl(INADDR_ANY);
     bool bound = false;
     const char* ba = std::getenv("CHANNEL_BOOTSTRAP_BIND_ANY");
-    if (!(ba && std::atoi(ba) == 1)) {
+    // a multi-node job (WORLD_SIZE > LOCAL_WORLD_SIZE) listens on every interface: its peers reach
+    // the master from other hosts, whatever MASTER_ADDR resolves to locally
+    const char* ws = std::getenv("WORLD_SIZE");
+    const char* lws = std::getenv("LOCAL_WORLD_SIZE");
+    const bool multinode = ws && lws && std::atoi(ws) > std::atoi(lws);
+    if (!(ba && std::atoi(ba) == 1) && !multinode) {
       addrinfo hints{}, *res = nullptr;
       hints.ai_family = AF_INET;
       hints.ai_socktype = SOCK_STREAM;
@@ -92,10 +97,18 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
         sockaddr_in m = sa;
         m.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
         freeaddrinfo(res);
-        bound = ::bind(ls, reinterpret_cast<sockaddr*>(&m), sizeof(m)) == 0;
-        if (!bound)
-          std::fprintf(stderr, "[channel] bootstrap: cannot bind MASTER_ADDR %s; listening on every interface\n",
+        // a hostname that resolves to a loopback alias on the master only (127.0.1.1 through
+        // /etc/hosts) would accept local peers and refuse remote ones: listen on every interface
+        const bool loop_alias = (ntohl(m.sin_addr.s_addr) >> 24) == 127 && addr != "127.0.0.1" && addr != "localhost";
+        if (loop_alias) {
+          std::fprintf(stderr, "[channel] bootstrap: MASTER_ADDR %s resolves to a loopback address; listening on every interface\n",
                        addr.c_str());
+        } else {
+          bound = ::bind(ls, reinterpret_cast<sockaddr*>(&m), sizeof(m)) == 0;
+          if (!bound)
+            std::fprintf(stderr, "[channel] bootstrap: cannot bind MASTER_ADDR %s; listening on every interface\n",
+                         addr.c_str());
+        }
       }
     }
     CH_CHECK(bound || ::bind(ls, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0,

@@ -179,11 +179,14 @@ void Solver::alloc() {
   // faster: R = 7, 8 (1024x385x1024: 39.5 -> 35.8 ms/step); the plain layout stays at R = 5
   // (512x257x512: 7.37 vs 7.63) and R = 10 (2048x633x2048: 315 vs 323; profiles/r04/ab_layout_grids.txt)
   kzb_ = (!comm_ && p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
-  // (the x transforms address a blocked field with 32-bit byte offsets)
-  if (kzb_ && static_cast<unsigned long long>(spec_rows(kSpecKzBlock, p.NY)) * p.nkx_loc *
-                      ((p.nkz_loc + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock) * (fp64_ ? 16 : 8) >= (1ull << 32))
-    kzb_ = 0;
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
+  // (the x transforms address a blocked field with 32-bit byte offsets: above 4 GiB per field the
+  // plain layout is used, also when CHANNEL_SPEC_KZB=1 asks for the blocked one)
+  if (kzb_ && static_cast<unsigned long long>(spec_rows(kSpecKzBlock, p.NY)) * p.nkx_loc *
+                      ((p.nkz_loc + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock) * (fp64_ ? 16 : 8) >= (1ull << 32)) {
+    if (std::getenv("CHANNEL_SPEC_KZB")) std::fprintf(stderr, "[channel] CHANNEL_SPEC_KZB ignored: a blocked field would exceed 4 GiB\n");
+    kzb_ = 0;
+  }
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();
   spec_ = static_cast<size_t>(spec_rows(kzb_, p.NY)) * p.nkx_loc * nkzs_;
@@ -990,6 +993,7 @@ void Solver::a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bh
   const size_t nr_me = static_cast<size_t>(std::max(0, std::min(nr, p.ny_loc - r0)));
   std::vector<A2ABlock> ops;
   ops.reserve(static_cast<size_t>(nf) * (bhi - blo));
+  if (to_phys) bwd_blocks_issued_ += bhi - blo;  // (host-side count of issued backward block exchanges)
   for (int f = 0; f < nf; ++f)
     for (int b = blo; b < bhi; ++b) {
       ops.emplace_back();
@@ -1464,6 +1468,7 @@ void Solver::step(bool stats_for_next) {
   const bool warm = !comm_ || comm_warm_;
   if (use_graph_ && warm && !debug_sync_enabled() && !phase_timing_) {
     if (!gexec_[gi] && !graph_ok_[gi]) {
+      const long long blocks_saved = bwd_blocks_issued_;
       try {
         hipGraph_t g = nullptr;
         // thread-local capture with a communicator: RCCL's proxy thread keeps making HIP calls
@@ -1477,6 +1482,11 @@ void Solver::step(bool stats_for_next) {
         // substep has been recorded, to drive the cross-rank agreement below
         const char* tf = std::getenv("CHANNEL_TEST_CAPTURE_FAIL");
         const bool inject = tf && std::atoi(tf) == plan_.rank;
+        // capturing records the step without running it, but step_body() still updates the host
+        // pipeline state (presend_done_: which kx sub-blocks of substep 0 the coming step resends).
+        // A graph that is abandoned (here or after the cross-rank agreement below) must leave that
+        // state as it was, or this rank's eager step would exchange other blocks than its peers'.
+        presend_saved_ = presend_done_;
         HIP_CHECK(hipStreamBeginCapture(s_comp_, mode));
         try {
           capture_fail_test_ = inject;
@@ -1485,6 +1495,8 @@ void Solver::step(bool stats_for_next) {
         } catch (...) {
           capture_fail_test_ = false;
           end_failed_capture();
+          presend_done_ = presend_saved_;
+          bwd_blocks_issued_ = blocks_saved;
           throw;
         }
         HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
@@ -1522,6 +1534,8 @@ void Solver::step(bool stats_for_next) {
             gexec_[gi] = nullptr;
             std::cerr << "[channel] hipGraph capture failed on a peer rank: every rank runs eagerly\n";
           }
+          presend_done_ = presend_saved_;  // the dropped graph never ran its pre-send
+          bwd_blocks_issued_ = blocks_saved;
           use_graph_ = false;
         }
       }
@@ -1909,8 +1923,9 @@ void Solver::run(long nsteps, bool verbose) {
 
 // t_end without a host sync per step (which would drain the CPU's run-ahead of the GPU): (dt, time)
 // of every step is copied to pinned memory behind the step, and the decision after step s reads the
-// copy of step s-1, which has finished while step s runs.  Within three steps of t_end it reads the
-// device time synchronously, so the run still stops at the first step whose end time reaches t_end.
+// copy of step s-1, which has finished while step s runs.  When that time is within one step's
+// largest advance of t_end (dt_max, or dt_fixed when set) it reads the device time synchronously,
+// so the run still stops at the first step whose end time reaches t_end.
 bool Solver::t_end_reached() {
   if (!h_tdt_) {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_tdt_), 4 * sizeof(double), hipHostMallocDefault));

@@ -13,8 +13,10 @@ namespace channel {
 
 // R values the y-line kernels are instantiated for (64*R >= NY).
 int yline_supported_R(int NY);
-// K-SPEC line geometry for NY: R rows per lane on H waves per line (H = 2: lines over two waves,
-// 64 R H >= NY; CHANNEL_KSPEC_HALVES=0 keeps one wave per line)
+// K-SPEC line geometry for NY: R rows per lane on H waves per line.  Default H = 1 (one wave per
+// line, 64 R >= NY); CHANNEL_KSPEC_HALVES=1 opts in to lines over two waves (H = 2, 64 R H >= NY),
+// measured slower at the headline grid and checked against the oracle by
+// tests/test_solver_gpu.py::test_kspec_halves_matches_oracle
 void kspec_geometry(int NY, bool fp64, int& R, int& H);
 
 // Device copies of the per-row coefficient tables (lane-major, see yline_device.hpp).  H = 2: row

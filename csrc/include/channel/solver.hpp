@@ -131,6 +131,9 @@ class Solver {
   const YTablesDev& ytables() const { return ytab_; }
   // kx sub-blocks of the local spectral layout (1 = plain [y][kx_local][kz]; see nkb_)
   int kblocks() const { return nkb_; }
+  // backward-exchange kx sub-block groups issued so far (host count: the pipeline bookkeeping of
+  // the pre-send, checked by the capture-failure test)
+  long long bwd_blocks_issued() const { return bwd_blocks_issued_; }
   int spec_kzb() const { return kzb_; }  // spectral layout (spec_index)
   // abort every communicator (the per-axis split ones first: aborting the parent does not abort
   // communicators split from it), so no stream stays blocked in an exchange with a dead peer
@@ -251,6 +254,8 @@ class Solver {
   // inside its graph) or, after anything that recomputed the outputs (prepare()), eagerly before
   // the step.  presend_done_: that exchange has been issued for the next substep 0.
   bool presend_done_ = false;
+  bool presend_saved_ = false;  // presend_done_ before a step capture (restored if the graph is dropped)
+  long long bwd_blocks_issued_ = 0;
   int xnt_ = 0;  // non-temporal spectral accesses in the x transforms (XArgs::nt)
   bool kb_overlap() const { return nkb_ > 1 && comm_ != nullptr; }
   // Forward-path overlap (slab, kx sub-blocks): the last y chunk's forward exchange goes out block

@@ -38,11 +38,11 @@ int yline_supported_R(int NY) {
 
 void kspec_geometry(int NY, bool fp64, int& R, int& H) {
   // opt-in (CHANNEL_KSPEC_HALVES=1): measured slower than one wave per line at 1024x385x1024
-  // (6.85 vs 4.2 ms per K-SPEC; profiles/r04/README.md) and not yet oracle-exact inside K-SPEC
-  static const bool on = [] {
-    const char* e = std::getenv("CHANNEL_KSPEC_HALVES");
-    return e && std::atoi(e) == 1;
-  }();
+  // (6.85 vs 4.2 ms per K-SPEC; profiles/r04/README.md); solver-level oracle test:
+  // tests/test_solver_gpu.py::test_kspec_halves_matches_oracle
+  // (read per Solver: a test process can construct solvers with and without it)
+  const char* e = std::getenv("CHANNEL_KSPEC_HALVES");
+  const bool on = e && std::atoi(e) == 1;
   // two waves of R = 4 per line where one wave would need R = 5..8 (one wave per SIMD at more
   // than 256 registers); rows N-3 .. N-1 must share a half (the D1 wall closure)
   if (on && !fp64 && NY > 256 + 2 && NY <= 512) {

@@ -223,3 +223,21 @@ def test_capture_failure_agreement_falls_back_eagerly(native, monkeypatch, capfd
     assert "capture failure injected" in err and "step graph not captured" in err, err[-2000:]
     assert _same(ref, got)
     got[0].barrier()
+
+
+def test_capture_failure_keeps_presend_state(native, monkeypatch):
+    """With kx sub-blocks (CHANNEL_KBLOCKS=4) every step ends by pre-sending blocks 0 .. NB-2 of the
+    next substep 0, and substep 0 then exchanges only block NB-1.  A capture that fails part-way
+    records some of that bookkeeping without running it; the abandoned graph must leave it as it
+    was, so the eager steps that follow exchange exactly the blocks an eager-from-the-start run
+    does (on a multi-rank job a mismatch would pair different exchange sizes between ranks).  The
+    host count of issued backward block exchanges is compared, and the states bitwise."""
+    monkeypatch.setenv("CHANNEL_KBLOCKS", "4")
+    ref = _run(native, native.new_unique_id(), nsteps=4, graph=False)
+    assert ref[0].kblocks() == 4
+    n_ref = ref[0].bwd_blocks_issued()
+    monkeypatch.setenv("CHANNEL_TEST_CAPTURE_FAIL", "0")
+    got = _run(native, native.new_unique_id(), nsteps=4, graph=True)
+    assert not got[0].graph_active()
+    assert got[0].bwd_blocks_issued() == n_ref, (got[0].bwd_blocks_issued(), n_ref)
+    assert _same(ref, got)

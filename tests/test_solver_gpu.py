@@ -78,6 +78,33 @@ def test_gpu_matches_oracle_large_ny(native, precision, NY):
         assert rel(gU, o.U) < tolU, f"U step {it}: {rel(gU, o.U):.3e}"
 
 
+@pytest.mark.parametrize("NY", [289, 385, 449])
+def test_kspec_halves_matches_oracle(native, monkeypatch, NY):
+    """The opt-in two-wave K-SPEC lines (CHANNEL_KSPEC_HALVES=1: R = 4 on 2 x 64 lanes for
+    256 + 2 < NY <= 512, fp32 storage) against the fp64 oracle, at the tolerance of the one-wave
+    fp32 path of test_gpu_matches_oracle_large_ny."""
+    monkeypatch.setenv("CHANNEL_KSPEC_HALVES", "1")
+    NX, NZ, dt = 16, 9, 1e-4
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision="fp32", dt_fixed=dt, stats_every=0, log_every=0,
+              symmetry_every=0, ic="zero")
+    s = make_solver(native, **kw)
+    o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=dt)
+    phi, om = ora.random_state(o.plan, o.ops, seed=5, amp=0.05)
+    phi = phi.astype(np.complex64).astype(np.complex128)
+    om = om.astype(np.complex64).astype(np.complex128)
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    o.set_state(phi, om, U)
+    s.set_state(phi, om, U)
+    s.prepare()
+    for it in range(2):
+        o.step()
+        s.step(False)
+        gphi, gom, gU = s.get_state()
+        assert rel(gphi, o.phi) < 1e-4, f"phi step {it}: {rel(gphi, o.phi):.3e}"
+        assert rel(gom, o.om) < 1e-4, f"omega step {it}: {rel(gom, o.om):.3e}"
+        assert rel(gU, o.U) < 1e-5, f"U step {it}: {rel(gU, o.U):.3e}"
+
+
 def test_poiseuille_steady(native):
     """BASELINE config 1 on the GPU path: the laminar profile 1.35(1-y^2) is a steady state."""
     s = make_solver(native, NX=32, NY=33, NZ=17, Re=100.0, precision="fp64", ic="laminar", stats_every=0,
