@@ -147,6 +147,59 @@ torch::Tensor xfft_f(torch::Tensor phys, int Kx) {
   return spec;
 }
 
+// x transforms on the one-rank blocked spectral layout (spec_index, kzb = 8; tests): the variants the
+// headline grid runs -- plane tiles (fp32 NX = 512 / 1024), 16-byte accesses (even nkz),
+// non-temporal spectral accesses (nt) -- on planes y0 .. y0 + ny - 1 of F fields of `rows` planes.
+// specb: 1-D complex buffer of F * spec_rows(rows) * nkx * nkzs elements (nkzs = nkz rounded up to 8)
+torch::Tensor xfft_b_blocked(torch::Tensor specb, int F, int rows, int y0, int ny, int NX, int Kx, int nkz, int nt,
+                             int zero_mean_field) {
+  check_dev_tensor(specb, "specb");
+  const bool f64 = is_fp64_complex(specb);
+  const int nkx = 2 * Kx + 1, nkzs = (nkz + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock;
+  const long long fstride = static_cast<long long>(spec_rows(kSpecKzBlock, rows)) * nkx * nkzs;
+  TORCH_CHECK(specb.dim() == 1 && specb.numel() == F * fstride, "specb must hold F blocked fields");
+  TORCH_CHECK(y0 >= 0 && ny > 0 && y0 + ny <= rows, "plane range outside the fields");
+  auto phys = torch::zeros({F, ny, NX, nkz}, specb.options());
+  XArgs a;
+  a.NX = NX; a.nkx = nkx; a.Kx = Kx; a.nkz = nkz; a.ny = ny; a.nfields = F;
+  a.field_stride_spec = fstride;
+  a.field_stride_phys = static_cast<long long>(ny) * NX * nkz;
+  a.kzb = kSpecKzBlock; a.nkzs = nkzs; a.spec_y0 = y0; a.nt = nt;
+  a.zero_mean_field = zero_mean_field;
+  XSrc s;
+  s.base = specb.data_ptr();
+  s.nsrc = 1;
+  s.kx_start[0] = 0;
+  s.kx_start[1] = nkx;
+  xfft_backward(a, s, phys.data_ptr(), twiddles(NX, f64), f64, cur_stream());
+  return phys;
+}
+
+// forward counterpart: phys [F, ny, NX, nkz] -> planes y0 .. y0 + ny - 1 of specb (updated in place)
+torch::Tensor xfft_f_blocked(torch::Tensor phys, torch::Tensor specb, int rows, int y0, int Kx, int nt) {
+  check_dev_tensor(phys, "phys");
+  check_dev_tensor(specb, "specb");
+  const bool f64 = is_fp64_complex(phys);
+  TORCH_CHECK(phys.dim() == 4, "phys must be [F, ny, NX, nkz]");
+  const int F = phys.size(0), ny = phys.size(1), NX = phys.size(2), nkz = phys.size(3);
+  const int nkx = 2 * Kx + 1, nkzs = (nkz + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock;
+  const long long fstride = static_cast<long long>(spec_rows(kSpecKzBlock, rows)) * nkx * nkzs;
+  TORCH_CHECK(specb.dim() == 1 && specb.numel() == F * fstride && is_fp64_complex(specb) == f64, "specb mismatch");
+  TORCH_CHECK(y0 >= 0 && y0 + ny <= rows, "plane range outside the fields");
+  XArgs a;
+  a.NX = NX; a.nkx = nkx; a.Kx = Kx; a.nkz = nkz; a.ny = ny; a.nfields = F;
+  a.field_stride_spec = fstride;
+  a.field_stride_phys = static_cast<long long>(ny) * NX * nkz;
+  a.kzb = kSpecKzBlock; a.nkzs = nkzs; a.spec_y0 = y0; a.nt = nt;
+  XDst d;
+  d.base = specb.data_ptr();
+  d.ndst = 1;
+  d.kx_start[0] = 0;
+  d.kx_start[1] = nkx;
+  xfft_forward(a, phys.data_ptr(), d, twiddles(NX, f64), f64, cur_stream());
+  return specb;
+}
+
 // z physical stage (tests): fields [6, ny, NX, nkz] -> H [3, ny, NX, nkz], maxima [4]
 std::pair<torch::Tensor, torch::Tensor> zphys_op(torch::Tensor fields, int Nzp, torch::Tensor inv_dy, double cx, double cz) {
   check_dev_tensor(fields, "fields");
@@ -205,7 +258,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fft_c2c", &fft_c2c, "batched in-LDS C2C FFT along the last axis; dir=+1 inverse (unnormalised)");
   m.def("xfft_backward", &xfft_b);
   m.def("xfft_forward", &xfft_f);
+  m.def("xfft_backward_blocked", &xfft_b_blocked, py::arg("specb"), py::arg("F"), py::arg("rows"), py::arg("y0"),
+        py::arg("ny"), py::arg("NX"), py::arg("Kx"), py::arg("nkz"), py::arg("nt") = 0, py::arg("zero_mean_field") = -1);
+  m.def("xfft_forward_blocked", &xfft_f_blocked, py::arg("phys"), py::arg("specb"), py::arg("rows"), py::arg("y0"),
+        py::arg("Kx"), py::arg("nt") = 0);
   m.def("zphys", &zphys_op);
+  m.def("xfft_last_variant", [] { return xfft_last_variant(); },
+        "template arguments of the last x-transform launch (rocprofv3 kernel-name form)");
 
   // tensor views of a Solver's device buffers, attached to the _core Solver class
   py::object cls = core.attr("Solver");

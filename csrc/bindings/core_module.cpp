@@ -190,6 +190,7 @@ PYBIND11_MODULE(_core, m) {
       .def("stats", [](Solver& s) { return vec(s.stats()); })
       .def("kblocks", &Solver::kblocks)
       .def("bwd_blocks_issued", &Solver::bwd_blocks_issued)
+      .def("spec_kzb", &Solver::spec_kzb)
       .def("mean_profile", [](Solver& s) { return vec(s.mean_profile()); })
       .def("health", &Solver::health)
       .def("time", &Solver::time)

@@ -100,6 +100,31 @@ __device__ __forceinline__ T2 mul_mi(T2 d) {
   }
 }
 
+// a + w b with w = -i (forward) or +i (inverse), and a - w b.  fp32: ONE v_pk_add_f32 each, the
+// swap of b's halves and the sign riding on op_sel / neg (a separate mul_mi materialised the
+// swapped value with a v_xor + v_mov pair per complex before the add: ~100 VALU per 1024-point
+// z-stage row, tools/isa_mix.py)
+__device__ __forceinline__ float2 pk_add_swap_nhi(float2 a, float2 b) {  // (ax + by, ay - bx)
+  f2v_t r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(v2(a)), "v"(v2(b)));
+  return c2v(r);
+}
+__device__ __forceinline__ float2 pk_add_swap_nlo(float2 a, float2 b) {  // (ax - by, ay + bx)
+  f2v_t r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(v2(a)), "v"(v2(b)));
+  return c2v(r);
+}
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 add_w(T2 a, T2 b) {  // a + (-+i) b
+  if constexpr (sizeof(T2) == 8) return INV ? pk_add_swap_nlo(a, b) : pk_add_swap_nhi(a, b);
+  else return cadd(a, mul_mi<INV>(b));
+}
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 sub_w(T2 a, T2 b) {  // a - (-+i) b
+  if constexpr (sizeof(T2) == 8) return INV ? pk_add_swap_nhi(a, b) : pk_add_swap_nlo(a, b);
+  else return csub(a, mul_mi<INV>(b));
+}
+
 
 // padded LDS index of logical element p of a row
 __device__ __forceinline__ constexpr int fft_pidx(int p) { return p + (p >> 4); }
@@ -116,15 +141,59 @@ __device__ __forceinline__ void dft2(T2* v) {
   v[1] = csub(a, b);
 }
 
+// compile-time zero (the pruned inputs of a zero-padded first pass): after inlining the compiler
+// folds the test, so the butterflies below drop the terms instead of adding zeros through asm
+template <typename T2>
+__device__ __forceinline__ bool is_czero(T2 x) {
+  return __builtin_constant_p(x.x) && __builtin_constant_p(x.y) && x.x == 0 && x.y == 0;
+}
+
 template <bool INV, typename T2>
 __device__ __forceinline__ void dft4(T2* v) {
   const T2 a0 = cadd(v[0], v[2]), a1 = csub(v[0], v[2]);
   const T2 a2 = cadd(v[1], v[3]);
-  const T2 a3 = mul_mi<INV>(csub(v[1], v[3]));
+  T2 o1, o3;
+  if (is_czero(v[1])) {  // d = -v3
+    o1 = sub_w<INV>(a1, v[3]);
+    o3 = add_w<INV>(a1, v[3]);
+  } else if (is_czero(v[3])) {
+    o1 = add_w<INV>(a1, v[1]);
+    o3 = sub_w<INV>(a1, v[1]);
+  } else {
+    const T2 d = csub(v[1], v[3]);
+    o1 = add_w<INV>(a1, d);
+    o3 = sub_w<INV>(a1, d);
+  }
   v[0] = cadd(a0, a2);
-  v[1] = cadd(a1, a3);
+  v[1] = o1;
   v[2] = csub(a0, a2);
-  v[3] = csub(a1, a3);
+  v[3] = o3;
+}
+// dft4 whose input v[2] still has to be multiplied by w = -i (forward) / +i (inverse): the product
+// folds into the first butterfly
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft4_w2(T2* v) {
+  const T2 a0 = add_w<INV>(v[0], v[2]), a1 = sub_w<INV>(v[0], v[2]);
+  const T2 a2 = cadd(v[1], v[3]), d = csub(v[1], v[3]);
+  v[0] = cadd(a0, a2);
+  v[1] = add_w<INV>(a1, d);
+  v[2] = csub(a0, a2);
+  v[3] = sub_w<INV>(a1, d);
+}
+// x W_8^1 (forward sign; inverse: conjugate) = h (x + w x), x W_8^3 = -h (x - w x)
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 mul_w8_1(T2 x) {
+  using T = decltype(x.x);
+  const T h = static_cast<T>(0.70710678118654752440);
+  const T2 t = add_w<INV>(x, x);
+  return T2{h * t.x, h * t.y};
+}
+template <bool INV, typename T2>
+__device__ __forceinline__ T2 mul_w8_3(T2 x) {
+  using T = decltype(x.x);
+  const T h = static_cast<T>(-0.70710678118654752440);
+  const T2 t = sub_w<INV>(x, x);
+  return T2{h * t.x, h * t.y};
 }
 
 // DFT of length 4*Q computed as Q-point... (generic two-level decomposition R = 4 x S)
@@ -141,18 +210,19 @@ __device__ __forceinline__ void dft8(T2* v) {
     dft4<INV>(a[n2]);
   }
   // twiddles W8^(n2*k1) for n2 = 1
-  // k1=1: W8^1 = (h, -h) fwd ; k1=2: -i ; k1=3: W8^3 = (-h, -h)
-  {
-    T2 x = a[1][1];
-    a[1][1] = INV ? T2{h * (x.x - x.y), h * (x.x + x.y)} : T2{h * (x.x + x.y), h * (x.y - x.x)};
-    a[1][2] = mul_mi<INV>(a[1][2]);
-    x = a[1][3];
-    a[1][3] = INV ? T2{-h * (x.x + x.y), h * (x.x - x.y)} : T2{h * (x.y - x.x), -h * (x.x + x.y)};
-  }
+  // k1=1: W8^1 = (h, -h) fwd ; k1=2: -i (folded into the radix-2 below) ; k1=3: W8^3 = (-h, -h)
+  (void)h;
+  a[1][1] = mul_w8_1<INV>(a[1][1]);
+  a[1][3] = mul_w8_3<INV>(a[1][3]);
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {
-    v[k1] = cadd(a[0][k1], a[1][k1]);
-    v[k1 + 4] = csub(a[0][k1], a[1][k1]);
+    if (k1 == 2) {
+      v[2] = add_w<INV>(a[0][2], a[1][2]);
+      v[6] = sub_w<INV>(a[0][2], a[1][2]);
+    } else {
+      v[k1] = cadd(a[0][k1], a[1][k1]);
+      v[k1 + 4] = csub(a[0][k1], a[1][k1]);
+    }
   }
 }
 
@@ -173,18 +243,27 @@ __device__ __forceinline__ void dft16(T2* v) {
   const T sg = INV ? T(1) : T(-1);  // sign of the sine part
   const T cs[10] = {T(1), c1, h, s1, T(0), -s1, -h, -c1, T(-1), -c1};
   const T sn[10] = {T(0), s1, h, c1, T(1), c1, h, s1, T(0), -s1};
+  // m = 2, 6: h (x +- w x) (one packed add + one packed multiply); m = 4: w, folded into the
+  // second-stage butterfly of k1 = 2 (dft4_w2)
 #pragma unroll
   for (int n2 = 1; n2 < 4; ++n2)
 #pragma unroll
     for (int k1 = 1; k1 < 4; ++k1) {
       const int m = n2 * k1;
-      const T2 w{cs[m], sg * sn[m]};
-      a[n2][k1] = cmul(a[n2][k1], w);
+      if (m == 2) {
+        a[n2][k1] = mul_w8_1<INV>(a[n2][k1]);
+      } else if (m == 6) {
+        a[n2][k1] = mul_w8_3<INV>(a[n2][k1]);
+      } else if (m != 4) {
+        const T2 w{cs[m], sg * sn[m]};
+        a[n2][k1] = cmul(a[n2][k1], w);
+      }
     }
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {
     T2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
-    dft4<INV>(b);
+    if (k1 == 2) dft4_w2<INV>(b);
+    else dft4<INV>(b);
 #pragma unroll
     for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
   }
@@ -500,17 +579,22 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
   constexpr int NB = RW * Q;
   constexpr int B = (NB + TPR - 1) / TPR;
   static_assert(!ZB || NS == 1, "zero-band pruning applies to the first pass");
+  // Power-of-two lengths: every index split of a pass satisfies fft_pidx(a + b) = fft_pidx(a) +
+  // fft_pidx(b) (reads: a = j < Q, b = r Q; writes: a = base, b = r NS, with (a % 16) + (b % 16) <
+  // 16 for radix-16-first plans), so each butterfly column is ONE address register plus
+  // compile-time LDS offsets (the per-element p + (p >> 4) cost ~150 VALU per 1024-point z row)
+  constexpr bool LIN = (N & (N - 1)) == 0;
   T2 v[B][R];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int idx = lane + b * TPR;
     if (NB % TPR == 0 || idx < NB) {
       const int row = idx / Q, j = idx - row * Q;
-      const T2* p = buf + row * PITCH;
+      const T2* p = buf + row * PITCH + (LIN ? fft_pidx(j) : 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (ZB && zero_block<N, Q>(r)) v[b][r] = T2{0, 0};
-        else v[b][r] = p[fft_pidx(j + r * Q)];
+        else v[b][r] = LIN ? p[fft_pidx(r * Q)] : p[fft_pidx(j + r * Q)];
       }
     }
   }
@@ -528,12 +612,15 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
         }
       }
       dftR<R, INV>(v[b]);
-      T2* p = buf + row * PITCH;
       const int base = (j - k) * R + k;
+      T2* p = buf + row * PITCH + (LIN ? fft_pidx(base) : 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int pos = base + r * NS;
-        if (!TR || pos <= N / 3 || pos >= N - N / 3) p[fft_pidx(pos)] = v[b][r];
+        if (!TR || pos <= N / 3 || pos >= N - N / 3) {
+          if constexpr (LIN) p[fft_pidx(r * NS)] = v[b][r];
+          else p[fft_pidx(pos)] = v[b][r];
+        }
       }
     }
   }
@@ -570,8 +657,9 @@ template <int N, bool INV, typename T2>
 __device__ __forceinline__ void wave_pass_first_reg(T2* __restrict__ buf, T2 (&x)[FftPlan<N>::R0], int j) {
   constexpr int R = FftPlan<N>::R0;
   dftR<R, INV>(x);
+  T2* p = buf + fft_pidx(j * R);  // (j R + r, r < R = 16: one address register, immediate offsets)
 #pragma unroll
-  for (int r = 0; r < R; ++r) buf[fft_pidx(j * R + r)] = x[r];
+  for (int r = 0; r < R; ++r) p[r] = x[r];
 }
 // middle pass (the second of a three-pass plan) through LDS
 template <int N, int PITCH, bool INV, int TPR, typename T2>
@@ -587,10 +675,11 @@ __device__ __forceinline__ void wave_pass_last_reg(const T2* __restrict__ buf, c
   constexpr int R = FftLast<N>::R, NS = FftLast<N>::NS, B = NS / TPR;
   const T2* t = tw + FftLast<N>::TOFF;
   T2 v[B][R];
+  const T2* p = buf + fft_pidx(lane);  // (TPR b + r NS: multiples of 16 added to lane < 64)
 #pragma unroll
   for (int b = 0; b < B; ++b)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b][r] = buf[fft_pidx(lane + TPR * b + r * NS)];
+    for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(TPR * b + r * NS)];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int j = lane + TPR * b;

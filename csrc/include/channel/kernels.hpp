@@ -1,6 +1,8 @@
 // Host-side launchers for the HIP kernels (implemented in csrc/kernels/*.hip).
 #pragma once
 
+#include <string>
+
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -189,6 +191,8 @@ struct XArgs {
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
 // forward: [y][x][kz] -> spectral truncated kx (unnormalised)
 void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s);
+// template arguments of this thread's last x-transform launch, in rocprofv3's kernel-name form (tests)
+std::string& xfft_last_variant();
 
 struct ZArgs {
   int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;   // NX = local x count (rows = ny * NX)

@@ -9,6 +9,11 @@ using namespace dev;
 
 static void build_reg_twiddles(int n, bool fp64, void** out);
 
+std::string& xfft_last_variant() {
+  static thread_local std::string v;
+  return v;
+}
+
 void Twiddles::build(int n_, bool fp64_) {
   release();
   n = n_;

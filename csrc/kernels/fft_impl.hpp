@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "channel/common.hpp"
@@ -507,6 +508,16 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   }
 }
 
+// The template arguments of the last x-transform launch of this thread, as in the rocprofv3 kernel
+// names ("xfft_backward_kernel<1024, float, false, 1, 0, 2, 2>"): tests assert that they exercise
+// the variant the headline grid runs (profiles/r04/final2/kernel_stats_1024x385x1024.csv)
+std::string& xfft_last_variant();
+inline void xfft_note_variant(const char* k, int nn, bool f64, bool seg, int wide, int sm, int v, int sl) {
+  xfft_last_variant() = std::string(k) + "<" + std::to_string(nn) + ", " + (f64 ? "double" : "float") + ", " +
+                        (seg ? "true" : "false") + ", " + std::to_string(wide) + ", " + std::to_string(sm) + ", " +
+                        std::to_string(v) + ", " + std::to_string(sl) + ">";
+}
+
 // Persistent grid of a transform kernel: the resident capacity, or fewer blocks per CU when
 // CHANNEL_<NAME>_BPC sets it (A/B: room beside it for a concurrent kernel of the other stream)
 inline int persist_blocks(const void* kern, int threads, const char* env) {
@@ -555,6 +566,9 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
                               : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
+  xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
+                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : kSegFull) : (sm == kSegOne ? kSegOne : kSegFull), V,
+                    a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
 }
@@ -577,6 +591,8 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
                               : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
+  xfft_note_variant("xfft_forward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
+                    a.kzb ? kSegOne : (a.npseg > 1 ? kSegFull : sm), V, a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));

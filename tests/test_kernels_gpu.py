@@ -119,6 +119,64 @@ def test_xfft(native, NX, nkz, dtype):
     assert rel(back, s) < tol
 
 
+def _blocked_index(rows, nkx, nkz):
+    """Element offsets spec_index(kzb = 8) of (y, ikx, kz) in one blocked field (kernels.hpp):
+    [y / 8][line / 8][y % 8][line % 8], line = ikx * nkzs + kz, nkzs = nkz rounded up to 8."""
+    nkzs = -(-nkz // 8) * 8
+    lines = nkx * nkzs
+    y = np.arange(rows)[:, None, None]
+    line = np.arange(nkx)[None, :, None] * nkzs + np.arange(nkz)[None, None, :]
+    idx = (y // 8) * 8 * lines + (y % 8) * 8 + (line // 8) * 64 + line % 8
+    return idx, (-(-rows // 8) * 8) * lines
+
+
+# The headline grid (1024 x 385 x 1024 fp32, one rank) runs the blocked spectral layout with plane
+# tiles and 16-byte accesses: rocprofv3 names xfft_backward_kernel<1024, float, false, 1, 0, 2, 2> and
+# xfft_forward_kernel<1024, float, false, 1, 0, 2, 2> (profiles/r04/final2/kernel_stats_1024x385x1024.csv).
+# These cases run those instantiations (and the fp64 / odd-nkz / other-length variants of the same
+# layout) against NumPy, on a plane range that starts and ends inside 8-plane tiles, with the
+# non-temporal accesses on and off, and with field 4's mean line read as zero (omega_y's source).
+@pytest.mark.parametrize("NX,nkz,dtype,nt,variant", [
+    (1024, 342, torch.complex64, 1, "<1024, float, false, 1, 0, 2, 2>"),
+    (1024, 342, torch.complex64, 0, "<1024, float, false, 1, 0, 2, 2>"),
+    (1024, 341, torch.complex64, 1, "<1024, float, false, 1, 0, 1, 2>"),
+    (1024, 342, torch.complex128, 1, "<1024, double, false, 0, 0, 1, 1>"),
+    (512, 86, torch.complex64, 0, "<512, float, false, 1, 0, 2, 2>"),
+    (2048, 20, torch.complex64, 1, "<2048, float, false, 0, 0, 2, 1>"),
+    (768, 50, torch.complex64, 0, "<768, float, false, 0, 0, 2, 1>"),
+])
+def test_xfft_blocked_layout(native, NX, nkz, dtype, nt, variant):
+    rng = np.random.default_rng(NX + nkz)
+    Kx = NX // 3
+    nkx = 2 * Kx + 1
+    rows, y0, ny = 13, 3, 6
+    F = 6
+    s = rng.standard_normal((F, rows, nkx, nkz)) + 1j * rng.standard_normal((F, rows, nkx, nkz))
+    idx, fstride = _blocked_index(rows, nkx, nkz)
+    buf = np.zeros(F * fstride, complex)
+    for f in range(F):
+        buf[f * fstride + idx] = s[f]
+    bt = torch.tensor(buf, dtype=dtype, device=DEV)
+    phys = native.xfft_backward_blocked(bt, F, rows, y0, ny, NX, Kx, nkz, nt, 4)
+    assert native.xfft_last_variant() == "xfft_backward_kernel" + variant, native.xfft_last_variant()
+    pos = np.where(np.arange(nkx) <= Kx, np.arange(nkx), NX - (nkx - np.arange(nkx)))
+    full = np.zeros((F, ny, NX, nkz), complex)
+    full[:, :, pos, :] = s[:, y0:y0 + ny]
+    full[4, :, 0, 0] = 0.0  # zero_mean_field = 4: (kx 0, kz 0) reads as zero
+    ref = np.fft.ifft(full, axis=2) * NX
+    tol = 1e-12 if dtype == torch.complex128 else 3e-6
+    assert rel(phys.cpu().numpy(), ref) < tol
+    # forward into fields pre-filled with a sentinel: only planes y0 .. y0 + ny - 1 change
+    sent = torch.full((3 * fstride,), 7.0 + 7.0j, dtype=dtype, device=DEV)
+    out = native.xfft_forward_blocked(phys[:3].contiguous(), sent, rows, y0, Kx, nt)
+    assert native.xfft_last_variant() == "xfft_forward_kernel" + variant, native.xfft_last_variant()
+    got = out.cpu().numpy()
+    for f in range(3):
+        g = got[f * fstride + idx]
+        assert rel(g[y0:y0 + ny] / NX, s[f, y0:y0 + ny]) < tol, f
+        assert np.all(g[:y0] == 7.0 + 7.0j) and np.all(g[y0 + ny:] == 7.0 + 7.0j), f
+
+
 @pytest.mark.parametrize("NX,Nzp,dtype", [(32, 32, torch.complex128), (64, 128, torch.complex64),
                                           (16, 1024, torch.complex64), (16, 1024, torch.complex128),
                                           (32, 2048, torch.complex64), (8, 2048, torch.complex128),

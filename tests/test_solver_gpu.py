@@ -78,6 +78,71 @@ def test_gpu_matches_oracle_large_ny(native, precision, NY):
         assert rel(gU, o.U) < tolU, f"U step {it}: {rel(gU, o.U):.3e}"
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp64"])
+def test_blocked_layout_nx1024_matches_oracle(native, monkeypatch, precision):
+    """The one-rank blocked spectral layout forced on (CHANNEL_SPEC_KZB=1) at NX = 1024, the
+    headline's x length: fp32 runs the plane-tile x kernels with 16-byte accesses
+    (xfft_*_kernel<1024, float, false, 1, 0, 2, 2>), fp64 the one-plane tiles; both against the
+    dense fp64 oracle for 3 steps."""
+    monkeypatch.setenv("CHANNEL_SPEC_KZB", "1")
+    NX, NY, NZ, dt = 1024, 65, 33, 3e-4
+    kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision=precision, dt_fixed=dt, stats_every=0, log_every=0,
+              symmetry_every=0, ic="zero")
+    s = make_solver(native, **kw)
+    assert s.spec_kzb() == 8
+    o = ora.OracleSolver(NX, NY, NZ, Re=400.0, dt_fixed=dt)
+    phi, om = ora.random_state(o.plan, o.ops, seed=11, amp=0.3)
+    if precision == "fp32":
+        phi = phi.astype(np.complex64).astype(np.complex128)
+        om = om.astype(np.complex64).astype(np.complex128)
+    # fp32: the fp32 round-off of the physical-space product (~1e-7 of the peak) fills the modes the
+    # random state leaves near zero, and at |kx| up to 341 phi = D2 v - k^2 v weighs that noise by
+    # k^2 (measured 1.8e-4 over all modes at step 0): the fp32 bound is taken on the lines holding
+    # >= 1e-6 of the peak line energy, as in test_fp32_tracks_fp64_on_resolved_modes
+    tol, tolU = (1e-9, 1e-11) if precision == "fp64" else (1e-4, 1e-5)
+
+    def err(g, w):
+        if precision == "fp64":
+            return rel(g, w)
+        e = np.sum(np.abs(w) ** 2, axis=0)
+        keep = e >= 1e-6 * e.max()
+        return np.sqrt(np.sum(np.abs(g - w) ** 2, axis=0)[keep].sum() / e[keep].sum())
+
+    U = 0.75 * 1.8 * (1 - o.ops.y ** 2)
+    o.set_state(phi, om, U)
+    s.set_state(phi, om, U)
+    s.prepare()
+    for it in range(3):
+        o.step()
+        s.step(False)
+        gphi, gom, gU = s.get_state()
+        assert err(gphi, o.phi) < tol, f"phi step {it}: {err(gphi, o.phi):.3e} (all modes {rel(gphi, o.phi):.3e})"
+        assert err(gom, o.om) < tol, f"omega step {it}: {err(gom, o.om):.3e} (all modes {rel(gom, o.om):.3e})"
+        assert rel(gU, o.U) < tolU, f"U step {it}: {rel(gU, o.U):.3e}"
+
+
+def test_blocked_layout_equals_plain_headline_ny(native, monkeypatch):
+    """CHANNEL_SPEC_KZB=1 vs =0 at 1024 x 385 x 17 (the headline's NX and NY; R = 7): the layouts
+    change only addressing and tiling, so the states after 3 steps agree to fp32 round-off."""
+    kw = dict(NX=1024, NY=385, NZ=17, Re=20700.0, precision="fp32", ic="random", ic_amplitude=0.05, stats_every=0,
+              log_every=0, symmetry_every=0, dt_fixed=5e-4)
+    res = {}
+    for kzb in ("0", "1"):
+        monkeypatch.setenv("CHANNEL_SPEC_KZB", kzb)
+        s = make_solver(native, **kw)
+        assert s.spec_kzb() == (8 if kzb == "1" else 0)
+        s.init_ic()
+        s.prepare()
+        for _ in range(3):
+            s.step(False)
+        res[kzb] = s.get_state()
+        del s
+    for f in range(3):
+        a, b = res["1"][f], res["0"][f]
+        print(f"field {f}: bitwise {np.array_equal(a, b)}, rel {rel(a, b):.3e}")
+        assert rel(a, b) < 1e-6, f
+
+
 @pytest.mark.parametrize("NY", [289, 385, 449])
 def test_kspec_halves_matches_oracle(native, monkeypatch, NY):
     """The opt-in two-wave K-SPEC lines (CHANNEL_KSPEC_HALVES=1: R = 4 on 2 x 64 lanes for
