@@ -86,6 +86,15 @@ void install_crash_handler() {
   for (int sig : {SIGSEGV, SIGBUS, SIGABRT, SIGILL, SIGFPE}) signal(sig, crash_handler);
 }
 
+int hip_runtime_version() {
+  static const int v = [] {
+    int r = 0;
+    (void)hipRuntimeGetVersion(&r);
+    return r;
+  }();
+  return v;
+}
+
 bool debug_sync_enabled() { return g_debug_sync; }
 void set_debug_sync(bool on) { g_debug_sync = on; }
 bool g_lds_poison = [] {
@@ -275,11 +284,17 @@ void Solver::alloc() {
   ychunk_ = ystreams_ >= 2 ? std::max(2, planes_in(104)) : planes_in(144);  // (2048x633x2048: 2 planes, 300.8 vs 310.7 ms at 1)
   // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
   // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
-  ychunk_p_ = std::min(64, planes_in(144));  // (several chunks keep the exchange pipelined)
+  // (several chunks keep the exchange pipelined); two compute streams hold two chunks in flight,
+  // so each gets the P = 1 per-stream budget
+  ychunk_p_ = std::min(64, ystreams_ >= 2 ? planes_in(104) : planes_in(144));
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
   // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
   if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
+  if (comm_ && ystreams_ >= 2) {
+    HIP_CHECK(hipStreamCreateWithFlags(&s_comp2_, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_comp2_, hipEventDisableTiming));
+  }
   for (int i = 2; i < ystreams_; ++i) {
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -318,6 +333,10 @@ void Solver::free_all() {
   for (auto e : tev_pool_) (void)hipEventDestroy(e);
   for (auto e : ev_join_) (void)hipEventDestroy(e);
   for (auto st : s_extra_) (void)hipStreamDestroy(st);
+  if (s_comp2_) (void)hipStreamDestroy(s_comp2_);
+  if (ev_comp2_) (void)hipEventDestroy(ev_comp2_);
+  s_comp2_ = nullptr;
+  ev_comp2_ = nullptr;
   ev_join_.clear();
   s_extra_.clear();
   for (auto* v : {&ev_cb_, &ev_cc_, &ev_kb_, &ev_fb_})
@@ -1106,9 +1125,21 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
   };
   backward(0);
+  // chunks alternate between two compute streams (each chunk waits for its own backward exchange,
+  // which follows K-SPEC on the comm stream; chunks touch disjoint phys planes and exchange rows;
+  // the CFL maxima are atomic); phase timing keeps one stream so the stage times add up
+  // (not inside a stream capture on a HIP runtime older than 7.2: a process that imports torch
+  // binds torch's bundled HIP 7.0 runtime and RCCL (same sonames), and there a captured step with the
+  // second compute stream forked next to the RCCL exchanges segfaults in the runtime; eager steps and
+  // /opt/rocm's 7.2 runtime -- bench.py and the drivers are torch-free -- capture it fine)
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  if (s_comp2_) HIP_CHECK(hipStreamIsCapturing(s_comp_, &cst));
+  const bool two = s_comp2_ != nullptr && !phase_timing_ && nch > 1 &&
+                   (cst == hipStreamCaptureStatusNone || hip_runtime_version() >= 70200000);
   for (int k = 0; k < nch; ++k) {
     if (k + 1 < nch) backward(k + 1);
-    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_cb_[k], 0));
+    hipStream_t cs = (two && (k & 1)) ? s_comp2_ : s_comp_;
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_cb_[k], 0));
     const int y0 = k * ch, ny = std::max(0, std::min(ch, p.ny_loc - y0));
     if (ny > 0) {
       for (int c = 0; c < P; ++c)
@@ -1123,21 +1154,21 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
       xc.ny = ny;
       xc.nfields = 6;
       char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz_loc * esz_;
-      ev(1, false);
-      xfft_backward(xc, src, ph, tw_x_, fp64_, s_comp_);
-      ev(1, true);
+      ev(1, false, cs);
+      xfft_backward(xc, src, ph, tw_x_, fp64_, cs);
+      ev(1, true, cs);
       ZArgs zc = za0;
       zc.ny = ny;
       zc.y0 = p.y0 + y0;
-      ev(2, false);
-      zphys(zc, ph, tw_z_, fp64_, s_comp_);
-      ev(2, true);
+      ev(2, false, cs);
+      zphys(zc, ph, tw_z_, fp64_, cs);
+      ev(2, true, cs);
       xc.nfields = 3;
-      ev(3, false);
-      xfft_forward(xc, ph, dst, tw_x_, fp64_, s_comp_);
-      ev(3, true);
+      ev(3, false, cs);
+      xfft_forward(xc, ph, dst, tw_x_, fp64_, cs);
+      ev(3, true, cs);
     }
-    HIP_CHECK(hipEventRecord(ev_cc_[k], s_comp_));
+    HIP_CHECK(hipEventRecord(ev_cc_[k], cs));
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_cc_[k], 0));
     if (fsplit && k == nch - 1) {
       // forward-path overlap: the CFL maxima first (every z stage is done), then the last chunk's
@@ -1159,6 +1190,10 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     ev(4, false, s_comm_);
     a2a_slab_chunk(k, ch, false, 3);
     ev(4, true, s_comm_);
+  }
+  if (two) {  // join the second compute stream (also reached through the forward exchange)
+    HIP_CHECK(hipEventRecord(ev_comp2_, s_comp2_));
+    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_comp2_, 0));
   }
   if (fsplit) {
     if (n == 0) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_cfl_, 0));
@@ -1436,6 +1471,7 @@ void Solver::end_failed_capture() {
   if (junk) (void)hipGraphDestroy(junk);
   std::vector<hipStream_t> forked = {s_comm_};
   for (auto st : s_extra_) forked.push_back(st);
+  if (s_comp2_) forked.push_back(s_comp2_);
   for (auto st : forked) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {

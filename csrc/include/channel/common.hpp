@@ -28,6 +28,8 @@ struct Error : std::runtime_error {
 // Debug mode: synchronise after every launch so asynchronous faults are attributed to the kernel
 // that caused them (the reference's kernelCheck ran cudaGetLastError without a sync, check.cu:7).
 bool debug_sync_enabled();
+// version of the HIP runtime this process is bound to (hipRuntimeGetVersion; torch imports bring their own)
+int hip_runtime_version();
 void set_debug_sync(bool on);
 // LDS poison-fill debug mode (CHANNEL_LDS_POISON=1 or set_lds_poison): the hot kernels fill their
 // shared memory with NaN bit patterns before any use, so a read of an LDS slot that the kernel

@@ -126,8 +126,15 @@ __device__ __forceinline__ T2 sub_w(T2 a, T2 b) {  // a - (-+i) b
 }
 
 
-// padded LDS index of logical element p of a row
-__device__ __forceinline__ constexpr int fft_pidx(int p) { return p + (p >> 4); }
+// padded LDS index of logical element p of a row: one pad slot per 2^SH elements.  SH = 4 (the
+// default): the stride-16 stores of a radix-16 first pass are conflict-free for ds_write_b64 and a
+// contiguous 32-lane ds_read_b64 half meets one 2-way conflict (its 32 elements span 33 slots).
+// SH = 5 (the 1024-point z stage): contiguous 32-lane reads are conflict-free (2 LDS cycles instead
+// of 4) and the first pass's stride-16 stores take 2-way conflicts (8 cycles instead of 6), which
+// nets fewer LDS cycles where a transform reads more than it writes at stride 16.
+template <int SH = 4>
+__device__ __forceinline__ constexpr int fft_pidx_s(int p) { return p + (p >> SH); }
+__device__ __forceinline__ constexpr int fft_pidx(int p) { return fft_pidx_s<4>(p); }
 template <int N>
 struct FftPitch {
   static constexpr int value = N + N / 16 + (N >= 16 ? 0 : 1);
@@ -570,7 +577,7 @@ __host__ __device__ constexpr bool zero_block(int r) {
 }
 
 template <int N, int R, int NS, int RW, int PITCH, bool INV, int TPR = 64, bool ZB = false, bool TR = false,
-          typename T2>
+          int SH = 4, typename T2>
 __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
   // tw: this pass's [R-1][NS] twiddle table; ZB: first pass of a zero-band input (zero_block);
   // TR: last pass of a forward x transform whose outputs in the 2/3-rule band are discarded (not
@@ -583,6 +590,9 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
   // fft_pidx(b) (reads: a = j < Q, b = r Q; writes: a = base, b = r NS, with (a % 16) + (b % 16) <
   // 16 for radix-16-first plans), so each butterfly column is ONE address register plus
   // compile-time LDS offsets (the per-element p + (p >> 4) cost ~150 VALU per 1024-point z row)
+  // (SH = 5: the same holds with (a % 32) + (b % 32) < 32 for the z stage's plans, 16x16x4 and the
+  // half-length 8x8x8, checked case by case; other plans keep SH = 4)
+  static_assert(SH == 4 || N == 1024 || N == 512, "pad shift 5: the z stage's plans only");
   constexpr bool LIN = (N & (N - 1)) == 0;
   T2 v[B][R];
 #pragma unroll
@@ -590,11 +600,11 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
     const int idx = lane + b * TPR;
     if (NB % TPR == 0 || idx < NB) {
       const int row = idx / Q, j = idx - row * Q;
-      const T2* p = buf + row * PITCH + (LIN ? fft_pidx(j) : 0);
+      const T2* p = buf + row * PITCH + (LIN ? fft_pidx_s<SH>(j) : 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if (ZB && zero_block<N, Q>(r)) v[b][r] = T2{0, 0};
-        else v[b][r] = LIN ? p[fft_pidx(r * Q)] : p[fft_pidx(j + r * Q)];
+        else v[b][r] = LIN ? p[fft_pidx_s<SH>(r * Q)] : p[fft_pidx_s<SH>(j + r * Q)];
       }
     }
   }
@@ -613,13 +623,13 @@ __device__ __forceinline__ void wave_pass(T2* __restrict__ buf, const T2* __rest
       }
       dftR<R, INV>(v[b]);
       const int base = (j - k) * R + k;
-      T2* p = buf + row * PITCH + (LIN ? fft_pidx(base) : 0);
+      T2* p = buf + row * PITCH + (LIN ? fft_pidx_s<SH>(base) : 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int pos = base + r * NS;
         if (!TR || pos <= N / 3 || pos >= N - N / 3) {
-          if constexpr (LIN) p[fft_pidx(r * NS)] = v[b][r];
-          else p[fft_pidx(pos)] = v[b][r];
+          if constexpr (LIN) p[fft_pidx_s<SH>(r * NS)] = v[b][r];
+          else p[fft_pidx_s<SH>(pos)] = v[b][r];
         }
       }
     }
@@ -653,33 +663,65 @@ constexpr bool fft_reg_edges_ok() {
   return FftPlan<N>::R0 * TPR == N && FftPlan<N>::R1 > 1 && FftLast<N>::NS % TPR == 0;
 }
 // first pass (NS = 1) from registers: x[r] = element j + r N/R0 (j = lane); writes its output
-template <int N, bool INV, typename T2>
+template <int N, bool INV, int SH = 4, typename T2>
 __device__ __forceinline__ void wave_pass_first_reg(T2* __restrict__ buf, T2 (&x)[FftPlan<N>::R0], int j) {
   constexpr int R = FftPlan<N>::R0;
   dftR<R, INV>(x);
-  T2* p = buf + fft_pidx(j * R);  // (j R + r, r < R = 16: one address register, immediate offsets)
+  T2* p = buf + fft_pidx_s<SH>(j * R);  // (j R + r, r < R = 16: one address register, immediate offsets)
 #pragma unroll
   for (int r = 0; r < R; ++r) p[r] = x[r];
 }
 // middle pass (the second of a three-pass plan) through LDS
-template <int N, int PITCH, bool INV, int TPR, typename T2>
+template <int N, int PITCH, bool INV, int TPR, int SH = 4, typename T2>
 __device__ __forceinline__ void wave_pass_middle(T2* __restrict__ buf, const T2* __restrict__ tw, int lane) {
   using Pl = FftPlan<N>;
   static_assert(Pl::R2 > 1, "middle pass of a three-pass plan");
-  wave_pass<N, Pl::R1, Pl::R0, 1, PITCH, INV, TPR>(buf, tw, lane);
+  wave_pass<N, Pl::R1, Pl::R0, 1, PITCH, INV, TPR, false, false, SH>(buf, tw, lane);
+}
+// The same pass (one butterfly per lane: N / R1 == 64) with its twiddles held in registers: butterfly
+// j = lane uses W^(k r), k = lane % R0, for every row and both directions (twr, loaded once per
+// kernel by middle_twiddles), instead of R1 - 1 LDS reads per transform
+template <int N>
+struct MidTw {
+  static constexpr int R = FftPlan<N>::R1, NS = FftPlan<N>::R0;
+  static constexpr bool ok = N / R == 64 && FftPlan<N>::R2 > 1;
+};
+template <int N, typename T2>
+__device__ __forceinline__ void middle_twiddles(const T2* __restrict__ tw, T2 (&twr)[MidTw<N>::R - 1], int lane) {
+  constexpr int NS = MidTw<N>::NS;
+#pragma unroll
+  for (int r = 1; r < MidTw<N>::R; ++r) twr[r - 1] = tw[(r - 1) * NS + lane % NS];
+}
+template <int N, int PITCH, bool INV, int SH = 4, typename T2>
+__device__ __forceinline__ void wave_pass_middle_rt(T2* __restrict__ buf, const T2 (&twr)[MidTw<N>::R - 1], int lane) {
+  constexpr int R = MidTw<N>::R, NS = MidTw<N>::NS, Q = N / R;
+  static_assert(MidTw<N>::ok && (N & (N - 1)) == 0, "register-twiddle middle pass: one butterfly per lane");
+  T2 v[R];
+  const T2* p = buf + fft_pidx_s<SH>(lane);
+#pragma unroll
+  for (int r = 0; r < R; ++r) v[r] = p[fft_pidx_s<SH>(r * Q)];
+  row_sync<64>();
+#pragma unroll
+  for (int r = 1; r < R; ++r) v[r] = cmul_tw<INV>(v[r], twr[r - 1]);
+  dftR<R, INV>(v);
+  const int k = lane % NS, base = (lane - k) * R + k;
+  T2* q = buf + fft_pidx_s<SH>(base);
+#pragma unroll
+  for (int r = 0; r < R; ++r) q[fft_pidx_s<SH>(r * NS)] = v[r];
+  row_sync<64>();
 }
 // last pass into registers: out[b + r B] = element j + r NS, j = lane + TPR b, B = NS / TPR
-template <int N, bool INV, int TPR, typename T2>
+template <int N, bool INV, int TPR, int SH = 4, typename T2>
 __device__ __forceinline__ void wave_pass_last_reg(const T2* __restrict__ buf, const T2* __restrict__ tw,
                                                    T2 (&out)[N / TPR], int lane) {
   constexpr int R = FftLast<N>::R, NS = FftLast<N>::NS, B = NS / TPR;
   const T2* t = tw + FftLast<N>::TOFF;
   T2 v[B][R];
-  const T2* p = buf + fft_pidx(lane);  // (TPR b + r NS: multiples of 16 added to lane < 64)
+  const T2* p = buf + fft_pidx_s<SH>(lane);  // (TPR b + r NS: multiples of 64 added to lane < 64)
 #pragma unroll
   for (int b = 0; b < B; ++b)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx(TPR * b + r * NS)];
+    for (int r = 0; r < R; ++r) v[b][r] = p[fft_pidx_s<SH>(TPR * b + r * NS)];
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     const int j = lane + TPR * b;
@@ -692,13 +734,13 @@ __device__ __forceinline__ void wave_pass_last_reg(const T2* __restrict__ buf, c
 }
 
 // length-N/2 transform of HalfPlan<N>; htw points at the appended tables (post twiddles first)
-template <int N, int PITCH, bool INV, int TPR = 64, typename T2>
+template <int N, int PITCH, bool INV, int TPR = 64, int SH = 4, typename T2>
 __device__ __forceinline__ void wave_fft_half(T2* __restrict__ buf, const T2* __restrict__ htw, int lane) {
   using Hp = HalfPlan<N>;
   static_assert(Hp::ok, "no half plan for this length");
-  wave_pass<Hp::H, Hp::R0, 1, 1, PITCH, INV, TPR>(buf, htw, lane);
-  wave_pass<Hp::H, Hp::R1, Hp::R0, 1, PITCH, INV, TPR>(buf, htw + Hp::P2, lane);
-  wave_pass<Hp::H, Hp::R2, Hp::R0 * Hp::R1, 1, PITCH, INV, TPR>(buf, htw + Hp::P3, lane);
+  wave_pass<Hp::H, Hp::R0, 1, 1, PITCH, INV, TPR, false, false, SH>(buf, htw, lane);
+  wave_pass<Hp::H, Hp::R1, Hp::R0, 1, PITCH, INV, TPR, false, false, SH>(buf, htw + Hp::P2, lane);
+  wave_pass<Hp::H, Hp::R2, Hp::R0 * Hp::R1, 1, PITCH, INV, TPR, false, false, SH>(buf, htw + Hp::P3, lane);
 }
 
 

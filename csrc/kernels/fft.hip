@@ -21,11 +21,21 @@ void Twiddles::build(int n_, bool fp64_) {
   const double two_pi = 2.0 * std::acos(-1.0);
   // N-point tables, then the z stage's real-signal half-transform tables (HalfPlan<n>)
   const int sz0 = fft_twiddle_size(n);
-  const int sz = sz0 + fft_half_twiddle_size(n);
+  const int szh = fft_half_twiddle_size(n);
+  // n = 1024: the z stage's 4 x 16 x 16 tables follow (fft1024_4x16x16): [15][64] W_1024^(j r),
+  // then [15][4] W_64^(k r) = W_1024^(16 k r)
+  const int sz = sz0 + szh + (n == 1024 ? kR4TwSize : 0);
   std::vector<double2> h(sz, double2{1.0, 0.0});
   auto w = [&](int m) { return double2{std::cos(two_pi * m / n), -std::sin(two_pi * m / n)}; };
   fft_twiddle_fill(n, [&](int i, int m) { h[i] = w(m); });
   fft_half_twiddle_fill(n, [&](int i, int m) { h[sz0 + i] = w(m); });
+  if (n == 1024) {
+    const int o = sz0 + szh;
+    for (int r = 1; r < 16; ++r) {
+      for (int j = 0; j < 64; ++j) h[o + (r - 1) * 64 + j] = w(j * r);
+      for (int k = 0; k < 4; ++k) h[o + kR4Tw2 + (r - 1) * 4 + k] = w(16 * k * r);
+    }
+  }
   if (fp64) {
     HIP_CHECK(hipMalloc(&buf, sz * sizeof(double2)));
     HIP_CHECK(hipMemcpy(buf, h.data(), sz * sizeof(double2), hipMemcpyHostToDevice));

@@ -598,6 +598,86 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
                      static_cast<const T2*>(tw.buf));
 }
 
+// ---- 1024-point row transform, 4 x 16 x 16 (z stage, fp32) -----------------------------------
+// In and out in the row layout of the z stage (lane t, slot s: element t + 64 s), Stockham DIT:
+//  P1 (R = 4, NS = 1): butterfly j = t + 64 g takes slots g, g + 4, g + 8, g + 12 of lane t -- all in
+//     the lane's registers, no twiddles; output y1[4 t + 256 g + b] lands in slot 4 g + b;
+//  a 4 x 4 transpose of (lane row t / 16, slot index b) for each g, by v_permlane32_swap (row bit 1
+//     <-> b bit 1) and v_permlane16_swap (row bit 0 <-> b bit 0): lane u = a + 16 k2 then holds the
+//     16 inputs r = 4 g + c of the P2 butterfly j2 = 4 a + k2, in slot r;
+//  P2 (R = 16, NS = 4): twiddles W_64^(k2 r) (tw2, registers) and a radix-16 DFT; the outputs go to
+//     LDS positions 64 a + k2 + 4 r' (one pad slot per 64 elements: 65 a + k2 + 4 r', conflict-free
+//     for the stride-64 ds_write_b64 groups);
+//  P3 (R = 16, NS = 64): lane j3 reads j3 + 64 r (65 r + j3: contiguous, conflict-free), twiddles
+//     W_1024^(j3 r) (tw3 table in LDS), radix-16 DFT; output r' is element j3 + 64 r' (the layout of
+//     the input).
+// One LDS round trip per transform instead of two (the 16 x 16 x 4 plan's first and last passes
+// run in registers but its middle pass reads and writes LDS both ways), for +32 permlane moves.
+// tw3: [15][64] W_1024^(j r) then (kR4Tw2) [15][4] W_64^(k r), forward sign; INV conjugates.
+constexpr int kR4Tw2 = 15 * 64, kR4TwSize = 15 * 64 + 15 * 4;
+__device__ __forceinline__ void permlane32_swap_c(float2& a, float2& b) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  a = float2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  b = float2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+__device__ __forceinline__ void permlane16_swap_c(float2& a, float2& b) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  a = float2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  b = float2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+template <bool INV>
+__device__ __forceinline__ void fft1024_4x16x16(float2 (&x)[16], float2* __restrict__ buf, const float2 (&tw2)[15],
+                                                const float2* __restrict__ tw3, int lane) {
+  // P1: radix-4 inside the lane
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float2 v[4] = {x[g], x[g + 4], x[g + 8], x[g + 12]};
+    dft4<INV>(v);
+    float2 y[4] = {v[0], v[1], v[2], v[3]};
+    // slot 4 g + b holds output b (written after all four loads of this g: slots g + 4 r overlap)
+    x[g] = y[0];
+    x[g + 4] = y[1];
+    x[g + 8] = y[2];
+    x[g + 12] = y[3];
+  }
+  // (P1 left output b of group g in slot g + 4 b; the transpose below works on slot 4 g + b, so
+  // relabel: z[4 g + b] = x[g + 4 b])
+  float2 z[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) z[4 * g + b] = x[g + 4 * b];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    permlane32_swap_c(z[4 * g + 0], z[4 * g + 2]);
+    permlane32_swap_c(z[4 * g + 1], z[4 * g + 3]);
+    permlane16_swap_c(z[4 * g + 0], z[4 * g + 1]);
+    permlane16_swap_c(z[4 * g + 2], z[4 * g + 3]);
+  }
+  // P2: slot r = input r of butterfly 4 a + k2 (a = lane % 16, k2 = lane / 16)
+#pragma unroll
+  for (int r = 1; r < 16; ++r) z[r] = cmul_tw<INV>(z[r], tw2[r - 1]);
+  dft16<INV>(z);
+  {
+    float2* q = buf + 65 * (lane & 15) + (lane >> 4);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) q[4 * r] = z[r];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // P3: butterfly j3 = lane
+  {
+    const float2* p = buf + lane;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = p[65 * r];
+  }
+  __builtin_amdgcn_wave_barrier();  // (the reads precede the row's next writes)
+#pragma unroll
+  for (int r = 1; r < 16; ++r) x[r] = cmul_tw<INV>(x[r], tw3[(r - 1) * 64 + lane]);
+  dft16<INV>(x);
+}
+
 // ---- z-direction physical stage -------------------------------------------------------------
 __device__ __forceinline__ void atomic_max_pos(float* p, float v) {
   atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
@@ -629,11 +709,27 @@ constexpr int zphys_rows() {
 }
 
 template <int NZP, typename T, bool SEG, bool ZH = true, int TPRT = zphys_tpr<NZP>(sizeof(T)),
-          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 2>
-__global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
+          int ZWT = zphys_rows<NZP, T, TPRT>(), int WPE = 2, int ZF = 3>
+__global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu(WPE), target("no-load-store-opt"))) zphys_kernel(ZArgs a, typename C2<T>::type* fields,
                                                          const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
-  constexpr int PITCH = FftPitch<NZP>::value;
+  // register-edge transforms (first pass from and last pass into registers, fft_device.hpp) where
+  // one wave owns a row and the plan has one first-pass butterfly per lane (NZP = 1024: 16x16x4)
+  constexpr int kEP = (NZP + TPRT - 1) / TPRT, kMK = (NZP / 3 + 1 + TPRT - 1) / TPRT;
+  constexpr bool kRegEdge = TPRT == 64 && kEP == 16 && FftPlan<NZP>::R0 == 16 && FftPlan<NZP>::R2 > 1 &&
+                            fft_reg_edges_ok<NZP, 64>() && 2 * kMK <= 16;
+  // row layout: one pad slot per 32 elements for the fp32 register-edge rows (their LDS traffic is
+  // mostly contiguous 64-lane reads: conflict-free ds_read_b64, kept unmerged by the kernel's
+  // no-load-store-opt attribute), per 16 elsewhere (fft_pidx_s)
+  constexpr int SH = kRegEdge && sizeof(T) == 4 ? 5 : 4;
+  // ZF (fp32 register-edge rows): 0 = three passes 16 x 16 x 4, middle-pass twiddles from LDS;
+  // 1 = the same with those twiddles in registers; 2 = 4 x 16 x 16 with one LDS round trip
+  // (fft1024_4x16x16: pad one slot per 64 elements, its own twiddle tables after the half plan's)
+  // ZF = 3: the same plan, and H_z through it as a complex transform of (Hz, 0) (its outputs k < nkz
+  // are the spectrum directly: no mirror, no half-length plan, one LDS round trip)
+  constexpr bool kR4 = kRegEdge && sizeof(T) == 4 && NZP == 1024 && ZF >= 2;
+  constexpr bool kR4Hz = kR4 && ZF == 3;
+  constexpr int PITCH = kR4 ? 1040 : (SH == 5 ? NZP + NZP / 32 : FftPitch<NZP>::value);
   constexpr int TPR = TPRT;  // threads per row
   constexpr int NWB = ZWT * TPR / 64;     // waves per block
   constexpr int TPRF = TPR < 64 ? 64 : TPR;  // threads per transform call (one wave or a row)
@@ -644,7 +740,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   // real H_z: half-length complex transform + post twiddles (HalfPlan) where one exists
   using Hp = HalfPlan<NZP>;
   constexpr bool kHalf = ZH && Hp::ok;
-  constexpr int TSA = TS + (kHalf ? Hp::SIZE : 0);
+  constexpr int TSA = TS + ((kHalf || kR4) ? Hp::SIZE : 0) + (kR4 ? kR4TwSize : 0);
   __shared__ T2 tws[TSA];  // twiddles staged once per block: LDS latency instead of L2 in the passes
   __shared__ float red[4][NWB];
   // lane: wave lane (reductions); t: thread within the row; w: row within the block
@@ -726,11 +822,19 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   // exposed load latency (the one-shot launch exposed it once per row: with the
   // transforms skipped the stage still took 55 of its 88 us per 8-plane chunk).
   constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
-  // register-edge transforms (first pass from and last pass into registers, fft_device.hpp) where
-  // one wave owns a row and the plan has one first-pass butterfly per lane (NZP = 1024: 16x16x4)
-  constexpr bool kRegEdge = TPR == 64 && EP == 16 && FftPlan<NZP>::R0 == 16 && FftPlan<NZP>::R2 > 1 &&
-                            fft_reg_edges_ok<NZP, 64>() && 2 * MK <= 16;
   T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
+  // the middle pass's twiddles in registers (fp32 register-edge rows: 30 VGPRs against 15 LDS reads
+  // per transform; CHANNEL_ZMIDTW=0 keeps the LDS reads, A/B)
+  constexpr bool kMidReg = kRegEdge && MidTw<NZP>::ok && sizeof(T) == 4 && ZF == 1;
+  T2 twm[kMidReg || kR4 ? 15 : 1];
+  if constexpr (kMidReg) middle_twiddles<NZP>(tws, twm, lane);
+  // 4 x 16 x 16: the second pass's twiddles W_64^(k2 r), k2 = lane / 16, in registers; the third
+  // pass's W_1024^(lane r) are read from the LDS table
+  const T2* tw3 = tws + TS + Hp::SIZE;  // (Twiddles::build: after the half plan's tables at n = 1024)
+  if constexpr (kR4) {
+#pragma unroll
+    for (int r = 1; r < 16; ++r) twm[r - 1] = tw3[kR4Tw2 + (r - 1) * 4 + lane / 16];
+  }
   // (not kept: a second buffer issuing pair 2 two transforms ahead and the next row's pair 1 a
   // row ahead: 28 spilled VGPRs, 39.4 vs 37.7 ms/step, profiles/r03s3/ab_zphys_prefetch2.txt)
   long long g = blockIdx.x;
@@ -803,10 +907,17 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
           }
         }
         if (!(a.diag & 1)) {
-          wave_pass_first_reg<NZP, true>(row, x, t);
-          row_sync<64>();
-          wave_pass_middle<NZP, PITCH, true, 64>(row, twl, t);
-          wave_pass_last_reg<NZP, true, 64>(row, twl, ph[p], t);
+          if constexpr (kR4) {
+            fft1024_4x16x16<true>(x, row, twm, tw3, t);
+#pragma unroll
+            for (int i = 0; i < EP; ++i) ph[p][i] = x[i];
+          } else {
+            wave_pass_first_reg<NZP, true, SH>(row, x, t);
+            row_sync<64>();
+            if constexpr (kMidReg) wave_pass_middle_rt<NZP, PITCH, true, SH>(row, twm, t);
+            else wave_pass_middle<NZP, PITCH, true, 64, SH>(row, twl, t);
+            wave_pass_last_reg<NZP, true, 64, SH>(row, twl, ph[p], t);
+          }
         } else {
 #pragma unroll
           for (int i = 0; i < EP; ++i) ph[p][i] = x[i];
@@ -869,10 +980,17 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       // mode k = t + 64 i sits in lane 64 - t at slot 15 - i (lane 0: its own slot 16 - i)
       T2 z[EP];
       if (!(a.diag & 1)) {
-        wave_pass_first_reg<NZP, false>(row, hxy, t);
-        row_sync<64>();
-        wave_pass_middle<NZP, PITCH, false, 64>(row, twl, t);
-        wave_pass_last_reg<NZP, false, 64>(row, twl, z, t);
+        if constexpr (kR4) {
+#pragma unroll
+          for (int i = 0; i < EP; ++i) z[i] = hxy[i];
+          fft1024_4x16x16<false>(z, row, twm, tw3, t);
+        } else {
+          wave_pass_first_reg<NZP, false, SH>(row, hxy, t);
+          row_sync<64>();
+          if constexpr (kMidReg) wave_pass_middle_rt<NZP, PITCH, false, SH>(row, twm, t);
+          else wave_pass_middle<NZP, PITCH, false, 64, SH>(row, twl, t);
+          wave_pass_last_reg<NZP, false, 64, SH>(row, twl, z, t);
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < EP; ++i) z[i] = hxy[i];
@@ -921,25 +1039,36 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       if (more) fetch(rnext, 0, pa, pb);
     }
     row_sync<TPRF>();
-    if constexpr (kHalf) {
+    if constexpr (kR4Hz) {
+      T2 zh[EP];
+#pragma unroll
+      for (int i = 0; i < EP; ++i) zh[i] = T2{hz[i], T(0)};
+      if (!(a.diag & 1)) fft1024_4x16x16<false>(zh, row, twm, tw3, t);
+      const T s2 = 2 * sc;  // (sc carries the 1/2 of the Hx / Hy split)
+#pragma unroll
+      for (int i = 0; i < MKO; ++i) {
+        const int k = t + TPR * i;
+        if (k < nkz && rv) zstore(2, zaddr(r, k), T2{zh[i].x * s2, zh[i].y * s2});
+      }
+    } else if constexpr (kHalf) {
       // H_z is real: z_m = Hz_2m + i Hz_2m+1 (scalar LDS stores, conflict-free), an N/2-point
       // transform, then Hz_k = E_k + W_N^k O_k (one N-point complex transform per row saved)
       T* rowf = reinterpret_cast<T*>(row);
 #pragma unroll
       for (int i = 0; i < EP; ++i) {
         const int n = t + TPR * i;
-        if (n < NZP) rowf[2 * fft_pidx(n >> 1) + (n & 1)] = hz[i];
+        if (n < NZP) rowf[2 * fft_pidx_s<SH>(n >> 1) + (n & 1)] = hz[i];
       }
       row_sync<TPRF>();
       const T2* htw = twl + TS;
-      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPRF>(row, htw, ft);
+      if (!(a.diag & 1)) wave_fft_half<NZP, PITCH, false, TPRF, SH>(row, htw, ft);
       T2 z0[MKO] = {}, z1[MKO] = {}, wk[MKO] = {};
 #pragma unroll
       for (int i = 0; i < MKO; ++i) {
         const int k = t + TPR * i;
         if (k < nkz) {
-          z0[i] = row[fft_pidx(k)];
-          z1[i] = row[fft_pidx((Hp::H - k) & (Hp::H - 1))];
+          z0[i] = row[fft_pidx_s<SH>(k)];
+          z1[i] = row[fft_pidx_s<SH>((Hp::H - k) & (Hp::H - 1))];
           wk[i] = htw[k];
         }
       }
@@ -1246,6 +1375,18 @@ inline bool zreg_enabled() {
   return on;
 }
 
+// CHANNEL_ZFFT = 0 | 1 | 2 | 3: the 1024-point fp32 z-stage row transforms (zphys_kernel ZF, A/B).
+// Default 3 (4 x 16 x 16 for all five transforms of a row); measured per 8-plane chunk alone at
+// 1024x385x1024: 60.9 / 58.5 / 57.9 / 56.9 us, bench 33.13 (ZF 1) / 32.97 / 32.79 ms/step
+// (gpurun_out/g10_*, profiles/r05/zfft_ab.txt)
+inline int zfft_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("CHANNEL_ZFFT");
+    return e ? std::atoi(e) : 3;
+  }();
+  return v;
+}
+
 // CHANNEL_ZHALF=0: H_z through a full-length complex transform (A/B of the half-length path)
 inline bool zhalf_enabled() {
   static const bool on = [] {
@@ -1274,6 +1415,12 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
                    static_cast<unsigned long long>(nrows) * a.nkz * sizeof(T2) >= (1ull << 32);
   auto kern = seg ? (zh ? zphys_kernel<NN, T, true, true, TPR, ZR, WPE> : zphys_kernel<NN, T, true, false, TPR, ZR, WPE>)
                   : (zh ? zphys_kernel<NN, T, false, true, TPR, ZR, WPE> : zphys_kernel<NN, T, false, false, TPR, ZR, WPE>);
+  if constexpr (sizeof(T) == 4 && NN == 1024 && TPR == 64 && WPE == 2) {
+    const int zf = zfft_mode();
+    if (!seg && zh && zf == 0) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 0>;
+    if (!seg && zh && zf == 1) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 1>;
+    if (!seg && zh && zf == 2) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 2>;
+  }
   const long long ngroups = (nrows + ZR - 1) / ZR;
   const long long cap = zpers_enabled() ? persist_blocks(reinterpret_cast<const void*>(kern), ZR * TPR, "CHANNEL_Z_BPC") : ngroups;
   dim3 grid(static_cast<unsigned>(std::min(ngroups, cap)));
