@@ -284,14 +284,17 @@ void Solver::alloc() {
   ychunk_ = ystreams_ >= 2 ? std::max(2, planes_in(104)) : planes_in(144);  // (2048x633x2048: 2 planes, 300.8 vs 310.7 ms at 1)
   // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
   // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
-  // (several chunks keep the exchange pipelined); two compute streams hold two chunks in flight,
-  // so each gets the P = 1 per-stream budget
-  ychunk_p_ = std::min(64, ystreams_ >= 2 ? planes_in(104) : planes_in(144));
+  // (several chunks keep the exchange pipelined); CHANNEL_PSTREAMS=2 alternates the chunks between
+  // two compute streams (opt-in: measured slower with a 1-rank RCCL communicator at the headline,
+  // 45.0 vs 43.1 ms/step with 6- vs 8-plane chunks, gpurun_out/g12_fc*.log), each then with the P = 1
+  // per-stream budget
+  if (const char* ps = std::getenv("CHANNEL_PSTREAMS")) pstreams_ = std::max(1, std::min(2, std::atoi(ps)));
+  ychunk_p_ = std::min(64, pstreams_ >= 2 ? planes_in(104) : planes_in(144));
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
   // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
   if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
-  if (comm_ && ystreams_ >= 2) {
+  if (comm_ && pstreams_ >= 2) {
     HIP_CHECK(hipStreamCreateWithFlags(&s_comp2_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&ev_comp2_, hipEventDisableTiming));
   }

@@ -226,10 +226,11 @@ class Solver {
   bool kprof_on_ = false;
   int ystreams_ = 1;               // streams the y chunks alternate over (P = 1)
   std::vector<hipStream_t> s_extra_;   // streams beyond compute + comm for the chunk pipeline
-  // P > 1 slab: a second compute stream; the y chunks' transforms alternate between s_comp_ and it
-  // (the comm stream carries the exchanges), as the P = 1 chunks alternate between two streams
+  // P > 1 slab, CHANNEL_PSTREAMS=2: a second compute stream; the y chunks' transforms alternate
+  // between s_comp_ and it (the comm stream carries the exchanges), as the P = 1 chunks do
   hipStream_t s_comp2_ = nullptr;
   hipEvent_t ev_comp2_ = nullptr;
+  int pstreams_ = 1;  // compute streams of the P > 1 chunk pipeline (CHANNEL_PSTREAMS)
   std::vector<hipEvent_t> ev_join_;
   int ychunk_ = 0;                 // y planes per x->z->x pipeline chunk (P = 1), 0 = whole slab
   double* d_invdy_ = nullptr;

@@ -277,11 +277,15 @@ template <int R, typename T, int W, int H = 1>
 constexpr int kspec_lds_tables_doubles() {
   return kYTabRowTables * 64 * R * H + PFac<R>::kNumFields * 64 * H + (H == 2 ? 64 * R * H : 0);
 }
-// stage the tables when tables + two tiles + the exchange scratch fit the 160 KB LDS
+// stage the tables when tables + two tiles + the exchange scratch fit the 160 KB LDS; fp64 storage
+// from R = 8 (whose double tiles alone take 82-102 KB): tables + ONE tile, the tables' per-row reads
+// from LDS instead of L2 (read from global memory they were hoisted into registers: 74 / 143 spilled
+// VGPRs at R = 8 / 10)
 template <int R, typename T, int W, int H = 1>
 constexpr bool kspec_tables_in_lds() {
+  constexpr int tiles = (sizeof(T) == 8 && R >= 8) ? 1 : 2;
   return kspec_lds_tables_doubles<R, T, W, H>() * 8 +
-             2 * Stage<R, T, W, 1, false, H>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+             tiles * Stage<R, T, W, 1, false, H>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
              kspec_scratch_doubles<R, W, H>() * 8 <=
          158 * 1024;
 }

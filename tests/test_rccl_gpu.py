@@ -241,3 +241,17 @@ def test_capture_failure_keeps_presend_state(native, monkeypatch):
     assert not got[0].graph_active()
     assert got[0].bwd_blocks_issued() == n_ref, (got[0].bwd_blocks_issued(), n_ref)
     assert _same(ref, got)
+
+
+def test_rccl_two_compute_streams_bitwise(native, monkeypatch):
+    """CHANNEL_PSTREAMS=2: the y chunks of the P > 1 pipeline alternate between two compute streams
+    (each chunk waits for its own backward exchange; the forward exchange of chunk k waits for the
+    stream that ran it).  Eager steps (inside a capture the second stream is used only on HIP
+    runtimes >= 7.2, i.e. not in a torch process: see transforms_slab) are bitwise the fast path."""
+    monkeypatch.setenv("CHANNEL_PSTREAMS", "2")
+    monkeypatch.setenv("CHANNEL_YCHUNK", "16")
+    ref = _run(native, b"")
+    got = _run(native, native.new_unique_id(), graph=False)
+    assert _same(ref, got)
+    got2 = _run(native, native.new_unique_id(), graph=True)
+    assert _same(ref, got2)

@@ -47,7 +47,7 @@ def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
 
 
 @pytest.mark.parametrize("precision,NY", [("fp32", 129), ("fp64", 129), ("fp32", 225), ("fp64", 225), ("fp32", 257),
-                                          ("fp64", 257), ("fp32", 385),
+                                          ("fp64", 257), ("fp32", 385), ("fp64", 481),
                                           ("fp32", 633), ("fp64", 633), ("fp32", 769), ("fp32", 1201),
                                           ("fp64", 1409)])
 def test_gpu_matches_oracle_large_ny(native, precision, NY):
@@ -488,6 +488,38 @@ def test_fp32_tracks_fp64_on_resolved_modes(native):
     print(f"U: rel {dU:.3e}")
     assert worst["phi"] < 2e-5 and worst["omega"] < 2e-5, worst
     assert dU < 1e-6
+
+
+def test_fp32_high_band_energy_bounded(native):
+    """fp32 storage round-off in the wavenumber bands the band-limited random IC leaves empty
+    (README, "fp32 storage and the high wavenumbers"; headline time series in
+    profiles/r05/highband_1024x385x1024_table.txt): from the same IC, 400 steps of fp32 and fp64
+    storage at 128 x 129 x 128 (Re = 3130), kinetic energy at three planes.  In the bands the IC
+    leaves empty (kz >= nkz/2, |kx| >= Kx/2) fp32 may only carry noise at the level of fp32
+    round-off (<= 1e-12 of the energy, ~300 eps^2) or the physical content fp64 finds there, and
+    the energy itself and the filled low band must agree."""
+    kw = dict(NX=128, NY=129, NZ=65, Re=3130.0, ic="random", ic_amplitude=0.05, stats_every=0, log_every=0,
+              symmetry_every=0, dt_fixed=2e-3, spectra_planes="3,16,64")
+    res = {}
+    for prec in ("fp64", "fp32"):
+        s = make_solver(native, precision=prec, **kw)
+        s.init_ic()
+        s.prepare()
+        for _ in range(400):
+            s.step(False)
+        assert s.health() == 0
+        sp = s.spectra()
+        ekz = np.asarray(sp["ekz"]).sum(axis=(0, 1))
+        ekx = np.asarray(sp["ekx"]).sum(axis=(0, 1))
+        res[prec] = (ekz.sum(), ekz[ekz.size // 2:].sum() / ekz.sum(), ekx[ekx.size // 2:].sum() / ekx.sum(),
+                     ekz[:8].sum() / ekz.sum())
+        del s
+    (E64, z64, x64, lo64), (E32, z32, x32, lo32) = res["fp64"], res["fp32"]
+    print(f"E {E32:.6e} / {E64:.6e}; kz>=nkz/2 {z32:.3e} / {z64:.3e}; kx>=Kx/2 {x32:.3e} / {x64:.3e}")
+    assert abs(E32 - E64) <= 1e-4 * E64
+    assert abs(lo32 - lo64) <= 1e-4
+    assert z32 <= max(100 * z64, 1e-12), (z32, z64)
+    assert x32 <= max(100 * x64, 1e-12), (x32, x64)
 
 
 @pytest.mark.parametrize("precision,NX,NY,NZ", [("fp32", 32, 33, 17), ("fp32", 64, 385, 33), ("fp64", 32, 129, 17),
