@@ -255,3 +255,39 @@ def test_rccl_two_compute_streams_bitwise(native, monkeypatch):
     assert _same(ref, got)
     got2 = _run(native, native.new_unique_id(), graph=True)
     assert _same(ref, got2)
+
+
+PSTREAMS_SCRIPT = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.environ["CHANNEL_ROOT"])
+from channel_gpu_amd import require_core
+from channel_gpu_amd.utils.config import default_config
+C = require_core()
+kw = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
+          log_every=0, symmetry_every=0)
+out = []
+for uid in (b"", C.new_unique_id()):
+    s = C.Solver(default_config(**kw), 0, 1, 0, uid)
+    s.init_ic(); s.prepare()
+    for _ in range(4):
+        s.step(False)
+    out.append((s.get_state(), s.graph_active(), s.comm_kind()))
+(a, ga, ka), (b, gb, kb) = out
+assert ka == "none" and kb == "rccl" and gb, (ka, kb, gb)
+assert all(np.array_equal(x, y) for x, y in zip(a, b))
+print("PSTREAMS_OK", flush=True)
+"""
+
+
+def test_rccl_two_compute_streams_captured_torch_free(native):
+    """CHANNEL_PSTREAMS=2 inside the captured step graph, in a torch-free process (ROCm 7.2's
+    runtime and RCCL, like bench.py and the drivers), bitwise the fast path."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CHANNEL_TORCH_FREE="1", CHANNEL_PSTREAMS="2", CHANNEL_YCHUNK="16", CHANNEL_ROOT=root)
+    r = subprocess.run([sys.executable, "-c", PSTREAMS_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "PSTREAMS_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
