@@ -144,6 +144,23 @@ template <typename T2, int V>
 struct alignas(sizeof(T2) * V) CVec {
   T2 c[V];
 };
+// Lane map of the global<->LDS transposes of the 16-column plane tiles (SL = 2, two planes x one
+// 8-wide kz block, V = 2): a ds_write_b64 is banked per 16 contiguous lanes modulo 32 dwords and a
+// ds_read_b64 per 32 lanes modulo 64, so no row pitch serves both with the same lane map (pitch
+// = 1 mod 16: writes conflict-free, reads 2-way; = 2 mod 16: the reverse).  With the pitch at
+// 2 mod 16 the global->LDS side takes quads of 4 lanes = one plane's 64-B kz piece, 8 rows per
+// half-wave, plane 0 in lanes 0-31 and plane 1 in 32-63 (16 lanes = 4 rows x 4 kz pairs of one
+// plane: conflict-free), and the LDS->global side keeps 8 lanes per row (2 planes x 4 kz pairs,
+// 4 rows per half-wave: conflict-free).  quad_col / quad_row: the column pair and the row of
+// thread tid within each group of NT / 8 rows.
+template <int NX, typename T, int WIDE, int SL, int V>
+struct XQuad {
+  static constexpr bool on = SL == 2 && V == 2 && XCfg<NX, T, WIDE>::C == 16 && FftPitch<NX>::value % 16 == 0;
+  static constexpr int PITCH = on ? FftPitch<NX>::value + 2 : XCfg<NX, T, WIDE>::PITCH;
+};
+__device__ __forceinline__ int quad_col(int tid) { return (tid & 3) | ((tid >> 3) & 4); }
+__device__ __forceinline__ int quad_row(int tid) { return ((tid >> 2) & 7) | ((tid >> 6) << 3); }
+
 // element at a 32-bit BYTE offset from a wave-uniform base: the global access then takes the base
 // in SGPRs and the offset in one VGPR (saddr form) instead of 64-bit address arithmetic per
 // element; every caller's span is checked below 4 GiB on the host
@@ -207,7 +224,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
   using CV = CVec<T2, V>;
-  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  using QM = XQuad<NX, T, WIDE, SL, V>;
+  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = QM::PITCH;
   constexpr int CW = C / V;  // accesses per tile row (V kz columns each; the host checks nkz % V == 0)
   // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
   constexpr int NKMAX = 2 * (NX / 3) + 1;
@@ -256,7 +274,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       // last accesses can pass it
       static_assert(NT % CW == 0, "a thread's column must be the same for every access");
       constexpr int DI = NT / CW;
-      const int c = (tid % CW) * V;
+      const int c = (QM::on ? quad_col(tid) : tid % CW) * V, r0 = QM::on ? quad_row(tid) : tid / CW;
       const unsigned bt = spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V)) *
                           static_cast<unsigned>(sizeof(T2));
       const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
@@ -264,14 +282,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       if (a.nt) {
 #pragma unroll
         for (int q = 0; q < EPT; ++q) {
-          int i = tid / CW + q * DI;
+          int i = r0 + q * DI;
           if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
           v[q] = ld_nt(at_byte(bv, bt + static_cast<unsigned>(i) * rs));
         }
       } else {
 #pragma unroll
         for (int q = 0; q < EPT; ++q) {
-          int i = tid / CW + q * DI;
+          int i = r0 + q * DI;
           if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
           v[q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
         }
@@ -315,9 +333,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int i = e / CW, c = (e - i * CW) * V;
+      const int i = QM::on ? quad_row(tid) + q * (NT / CW) : e / CW;
+      const int c = (QM::on ? quad_col(tid) : e - (e / CW) * CW) * V;
       const int x = i <= KXH ? i : NX - (NKX - i);
-      if (e < nload)
+      if (QM::on ? i < NKX : e < nload)
 #pragma unroll
         for (int u = 0; u < V; ++u)
           s[(c + u) * PITCH + fft_pidx(x)] = (zmean && i == 0 && (c + u) % KC == 0) ? T2{0, 0} : v[q].c[u];
@@ -376,9 +395,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
   using CV = CVec<T2, V>;
-  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = Cfg::PITCH;
+  using QM = XQuad<NX, T, WIDE, SL, V>;
+  constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = QM::PITCH;
   constexpr int CW = C / V;
   constexpr int EPT = (NX * CW + NT - 1) / NT;
+  static_assert(!QM::on || NT % CW == 0, "quad lane map: a thread's column is the same for every access");
   constexpr int NKX = 2 * (NX / 3) + 1, KXH = NX / 3;  // retained kx: the 2/3 rule's (checked on the host)
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
@@ -417,8 +438,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int x = min(e / CW, NX - 1);
-      const int c = (e % CW) * V;
+      const int x = min(QM::on ? quad_row(tid) + q * (NT / CW) : e / CW, NX - 1);
+      const int c = (QM::on ? quad_col(tid) : e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V), yy = min(y + c / KC, a.ny - 1);
       if constexpr (SEG) {
         const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
@@ -440,8 +461,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int x = e / CW, c = (e - x * CW) * V;
-      if (e < NX * CW)
+      const int x = QM::on ? quad_row(tid) + q * (NT / CW) : e / CW;
+      const int c = (QM::on ? quad_col(tid) : e - (e / CW) * CW) * V;
+      if (QM::on ? x < NX : e < NX * CW)
 #pragma unroll
         for (int u = 0; u < V; ++u) s[(c + u) * PITCH + fft_pidx(x)] = v[q].c[u];
     }

@@ -326,6 +326,11 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   constexpr int NTAB = kspec_lds_tables_doubles<R, T, W, H>();
   constexpr bool kDoubleTile = kspec_double_tile<R, T, W, H>();
   constexpr int XS = xl_scratch_doubles(kKspecXK + (H == 2 ? 1 : 0));  // (+ the spike column)
+  // LEAN: two waves per SIMD at R >= 5 (8 one-wave lines per workgroup, <= 256 registers): the
+  // multi-RHS solves run two real right-hand sides (one complex field) at a time on the same
+  // factorisation, so the 6- and 4-RHS working sets and their cross-lane temporaries are never
+  // live at once (CHANNEL_KSPEC_W8, A/B)
+  constexpr bool LEAN = H == 1 && W >= 8 && R >= 5;
   static_assert(H == 1 || (SPLIT == 0 && GLM == 0), "two-wave lines: the fused kernel");
   __shared__ double tab_lds[TLDS ? NTAB : 1];
   __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * St::TILE];
@@ -611,7 +616,21 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
         // (two-wave lines: each half factors its own rows, the coupling to the other half dropped)
         pfactor<R, XM>(F, CutLo<CoefImpl>{ci, H == 2 && hh == 1 && lane == 0}, xl, lane);
         constexpr int KS = H == 2 ? 1 : 0;  // + the half's spike right-hand side
-        {
+        if constexpr (LEAN) {
+          psolve<R, 2, XM>(F, ci, rhsW, xl, lane);
+          psolve<R, 2, XM>(F, ci, rhsP, xl, lane);
+          int zl = 0;  // (laundered: the loop-invariant unit columns would otherwise be hoisted)
+          asm volatile("" : "+v"(zl));
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int j = row(r) + zl;
+            pp[0][r] = rhsP[0][r];
+            pp[1][r] = rhsP[1][r];
+            pp[2][r] = (j == 0) ? 1.0 : 0.0;
+            pp[3][r] = (j == N - 1) ? 1.0 : 0.0;
+          }
+          psolve<R, 2, XM>(F, ci, *reinterpret_cast<double (*)[2][R]>(&pp[2][0]), xl, lane);
+        } else {
           // omega, phi and the two homogeneous phi solutions (k=0 -> phi(-1)=1, k=1 -> phi(+1)=1)
           // share the factorisation: one solve with 6 real right-hand sides
           double Z[6 + KS][R];
@@ -686,10 +705,18 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
         pfactor<R, XM>(F, CutLo<CoefHelm>{chm, H == 2 && hh == 1 && lane == 0}, xl, lane);
         constexpr int KS = H == 2 ? 1 : 0;
         double Y[4 + KS][R];  // v particular (0, 1), homogeneous v (2, 3) [, the half's spike]
-        apply_M<R, 4, XM>(t, pp, reinterpret_cast<double (&)[4][R]>(Y), lane, g);
-        if constexpr (H == 2) spike_rhs<R>(Y[4], chm, g, lane);
-        psolve<R, 4 + KS, XM>(F, chm, Y, xl, lane);
-        spike_join<R, 4, 4 + KS>(Y, Y[4 + KS - 1], g, lane);
+        if constexpr (LEAN) {
+          for (int hf = 0; hf < 2; ++hf) {  // (not unrolled: one copy of the solve)
+            double(&Yh)[2][R] = *reinterpret_cast<double (*)[2][R]>(&Y[2 * hf][0]);
+            apply_M<R, 2, XM>(t, *reinterpret_cast<const double (*)[2][R]>(&pp[2 * hf][0]), Yh, lane, g);
+            psolve<R, 2, XM>(F, chm, Yh, xl, lane);
+          }
+        } else {
+          apply_M<R, 4, XM>(t, pp, reinterpret_cast<double (&)[4][R]>(Y), lane, g);
+          if constexpr (H == 2) spike_rhs<R>(Y[4], chm, g, lane);
+          psolve<R, 4 + KS, XM>(F, chm, Y, xl, lane);
+          spike_join<R, 4, 4 + KS>(Y, Y[4 + KS - 1], g, lane);
+        }
         fresh();
         // wall derivatives v'(+-1) = first / last row of the dense D1 applied to v (no solves)
         double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -830,7 +857,14 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     // ---------------- prepare velocity / vorticity for the physical-space stage --------------
     fresh();
     double dvo[4][R];  // D1 v (0, 1), D1 omega (2, 3): one 4-RHS solve
-    d1_apply_to<R, 4, XM>(t, vo, dvo, xl, lane, g);
+    if constexpr (LEAN) {
+      d1_apply_to<R, 2, XM>(t, *reinterpret_cast<const double (*)[2][R]>(&vo[0][0]),
+                            *reinterpret_cast<double (*)[2][R]>(&dvo[0][0]), xl, lane, g);
+      d1_apply_to<R, 2, XM>(t, *reinterpret_cast<const double (*)[2][R]>(&vo[2][0]),
+                            *reinterpret_cast<double (*)[2][R]>(&dvo[2][0]), xl, lane, g);
+    } else {
+      d1_apply_to<R, 4, XM>(t, vo, dvo, xl, lane, g);
+    }
     KSPEC_STAMP(7)
     // velocities u = i (al dv - be om)/k2, w = i (be dv + al om)/k2 (nonLinear_kernels.cu:55-72),
     // formed one output at a time (each is stored before the next is built)
@@ -1159,6 +1193,16 @@ static int kspec_ns7() {
   return ns;
 }
 
+// CHANNEL_KSPEC_W8=1: the R = 7 fp32 kernel at 8 lines per workgroup, two waves per SIMD (LEAN
+// solves, async LDS staging instead of register slots; A/B against the one-wave-per-SIMD default)
+static bool kspec_w8() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_KSPEC_W8");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+
 // CHANNEL_KSPEC_VAR = w4 | ns2 (A/B at R = 3, the small grids): 4 lines per block instead of 8,
 // or two register prefetch slots instead of one
 static int kspec_var_env() {
@@ -1201,6 +1245,14 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   if constexpr (R == 7 && sizeof(T) == 4 && PAR == 0) {
     if (kspec_glds7()) kern = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
     if (kspec_ns7() == 3) kern = kspec_kernel<R, T, W, 3, kspec_xmode<R, T>(), PAR>;
+    if (kspec_w8()) {
+      constexpr int W8 = 8;
+      auto k = kspec_kernel<R, T, W8, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 1>;
+      const int nt = (a.lines + W8 - 1) / W8;
+      dim3 grid(std::min(nt, resident_blocks(reinterpret_cast<const void*>(k), W8 * 64))), block(W8 * 64);
+      hipLaunchKernelGGL(k, grid, block, 0, stream, t.tab, a);
+      return;
+    }
   }
   const int sp = kspec_split_env();
   if constexpr (kspec_split_default<R, T>()) {
