@@ -258,18 +258,18 @@ std::vector<int> Config::spectra_plane_list() const {
 }
 
 // transform lengths with kernels (kernels/fft.hip CH_DISPATCH_N): 2^k in [16, 2048], and m*2^k
-// (2^k >= 16, at most 2048 points) for m = 3, 5, 7, 9, 15 (the reference's cuFFT plans take any
-// length, fft.c:17-23)
+// (2^k >= 16, at most 2048 points) for m = 3, 5, 7, 9, 11, 13, 15 (the reference's cuFFT plans take
+// any length, fft.c:17-23)
 bool fft_length_supported(int n) {
   if (n < 16 || n > 2048) return false;
-  for (int m : {1, 3, 5, 7, 9, 15}) {
+  for (int m : {1, 3, 5, 7, 9, 11, 13, 15}) {
     if (n % m) continue;
     const int p = n / m;
     if ((p & (p - 1)) == 0 && p >= 16) return true;
   }
   return false;
 }
-static const char* kFftLengths = "2^k (16..2048) or 3, 5, 7, 9, 15 times 2^k >= 16 (at most 2048)";
+static const char* kFftLengths = "2^k (16..2048) or 3, 5, 7, 9, 11, 13, 15 times 2^k >= 16 (at most 2048)";
 
 void Config::validate() const {
   CH_CHECK(fft_length_supported(NX), "NX=" << NX << " must be " << kFftLengths);

@@ -96,7 +96,7 @@ struct Config {
   std::vector<int> spectra_plane_list() const;   // parsed spectra_planes (default {NY/2})
 };
 
-// FFT lengths the transform kernels are instantiated for: 2^k (16..2048) and 3, 5, 7, 9, 15 x 2^k
+// FFT lengths the transform kernels are instantiated for: 2^k (16..2048) and 3, 5, 7, 9, 11, 13, 15 x 2^k
 // (2^k >= 16, at most 2048 points)
 bool fft_length_supported(int n);
 

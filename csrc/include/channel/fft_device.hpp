@@ -336,34 +336,66 @@ struct RootTable<15> {
                                    -0.74314482547739423501, -0.40673664307580020775};
 };
 
-// radix 7 (forward sign; INV flips it): X_k = a_k - i b_k, X_{7-k} = a_k + i b_k with
-// a_k = v0 + sum_j cos(2 pi jk/7) (v_j + v_{7-j}), b_k = sum_j sin(2 pi jk/7) (v_j - v_{7-j})
-template <bool INV, typename T2>
-__device__ __forceinline__ void dft7(T2* v) {
+// odd prime radix P = 7, 11, 13 (forward sign; INV flips it): X_k = a_k - i b_k,
+// X_{P-k} = a_k + i b_k with a_k = v0 + sum_j cos(2 pi jk/P) (v_j + v_{P-j}),
+// b_k = sum_j sin(2 pi jk/P) (v_j - v_{P-j}), j, k = 1 .. (P-1)/2: (P-1)^2/2 real multiply-adds
+// per component instead of P^2
+template <int P, bool INV, typename T2>
+__device__ __forceinline__ void dft_odd(T2* v) {
   using T = decltype(v[0].x);
-  using RT = RootTable<7>;
-  T2 t[4], d[4];
+  using RT = RootTable<P>;
+  constexpr int H = (P - 1) / 2;
+  T2 t[H + 1], d[H + 1];
 #pragma unroll
-  for (int j = 1; j <= 3; ++j) {
-    t[j] = cadd(v[j], v[7 - j]);
-    d[j] = csub(v[j], v[7 - j]);
+  for (int j = 1; j <= H; ++j) {
+    t[j] = cadd(v[j], v[P - j]);
+    d[j] = csub(v[j], v[P - j]);
   }
   const T2 v0 = v[0];
-  v[0] = cadd(v0, cadd(t[1], cadd(t[2], t[3])));
+  T2 s0 = t[H];
 #pragma unroll
-  for (int k = 1; k <= 3; ++k) {
+  for (int j = H - 1; j >= 1; --j) s0 = cadd(t[j], s0);
+  v[0] = cadd(v0, s0);
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
     T2 a = v0, b{T(0), T(0)};
 #pragma unroll
-    for (int j = 1; j <= 3; ++j) {
-      const T c = static_cast<T>(RT::c[(j * k) % 7]), sn = static_cast<T>(RT::s[(j * k) % 7]);
+    for (int j = 1; j <= H; ++j) {
+      const T c = static_cast<T>(RT::c[(j * k) % P]), sn = static_cast<T>(RT::s[(j * k) % P]);
       a = T2{a.x + c * t[j].x, a.y + c * t[j].y};
       b = T2{b.x + sn * d[j].x, b.y + sn * d[j].y};
     }
     const T2 m = mul_mi<INV>(b);  // -i b (forward)
     v[k] = cadd(a, m);
-    v[7 - k] = csub(a, m);
+    v[P - k] = csub(a, m);
   }
 }
+template <bool INV, typename T2>
+__device__ __forceinline__ void dft7(T2* v) {
+  dft_odd<7, INV>(v);
+}
+template <>
+struct RootTable<11> {
+  static constexpr double c[11] = {1.0, 0.84125353283118120551, 0.41541501300188643508, -0.1423148382732850048,
+                                   -0.65486073394528498959, -0.95949297361449736865, -0.95949297361449736865,
+                                   -0.65486073394528498959, -0.1423148382732850048, 0.41541501300188643508,
+                                   0.84125353283118120551};
+  static constexpr double s[11] = {0.0, 0.54064081745559755543, 0.90963199535451833011, 0.98982144188093279524,
+                                   0.7557495743542582689, 0.28173255684142967104, -0.28173255684142967104,
+                                   -0.7557495743542582689, -0.98982144188093279524, -0.90963199535451833011,
+                                   -0.54064081745559755543};
+};
+template <>
+struct RootTable<13> {
+  static constexpr double c[13] = {1.0, 0.88545602565320991051, 0.56806474673115592289, 0.12053668025532300601,
+                                   -0.35460488704253545489, -0.74851074817110119231, -0.9709418174260520118,
+                                   -0.9709418174260520118, -0.74851074817110119231, -0.35460488704253545489,
+                                   0.12053668025532300601, 0.56806474673115592289, 0.88545602565320991051};
+  static constexpr double s[13] = {0.0, 0.46472317204376850652, 0.82298386589365635224, 0.99270887409805397272,
+                                   0.93501624268541483342, 0.66312265824079519305, 0.23931566428755768339,
+                                   -0.23931566428755768339, -0.66312265824079519305, -0.93501624268541483342,
+                                   -0.99270887409805397272, -0.82298386589365635224, -0.46472317204376850652};
+};
 template <>
 struct RootTable<6> {
   static constexpr double c[6] = {1.0, 0.5, -0.5, -1.0, -0.5, 0.5};
@@ -433,7 +465,9 @@ __device__ __forceinline__ void dftR(T2* v) {
   else if constexpr (R == 8) dft8<INV>(v);
   else if constexpr (R == 9) dft_ab<3, 3, INV>(v);
   else if constexpr (R == 10) dft_ab<5, 2, INV>(v);
+  else if constexpr (R == 11) dft_odd<11, INV>(v);
   else if constexpr (R == 12) dft_ab<4, 3, INV>(v);
+  else if constexpr (R == 13) dft_odd<13, INV>(v);
   else if constexpr (R == 15) dft_ab<5, 3, INV>(v);
   else {
     static_assert(R == 16, "unsupported radix");
@@ -448,7 +482,7 @@ struct Radices {
 };
 __host__ __device__ constexpr bool fft_radix_ok(int r) {
   return r == 1 || r == 2 || r == 3 || r == 4 || r == 5 || r == 6 || r == 7 || r == 8 || r == 9 || r == 10 ||
-         r == 12 || r == 15 || r == 16;
+         r == 11 || r == 12 || r == 13 || r == 15 || r == 16;
 }
 __host__ __device__ constexpr Radices fft_radices(int n) {
   if (n <= 16) return Radices{n, 1, 1};
@@ -458,9 +492,9 @@ __host__ __device__ constexpr Radices fft_radices(int n) {
   if (rem % 16 == 0 && fft_radix_ok(rem / 16)) return Radices{16, 16, rem / 16};
   const int odd = rem % 3 == 0 ? 3 : (rem % 5 == 0 ? 5 : 1);
   if (odd > 1 && fft_radix_ok(rem / odd)) return Radices{16, rem / odd, odd};
-  // 7 * 2^k, 9 * 2^k, 15 * 2^k: the whole odd factor in the last pass
-  const int odds[3] = {7, 9, 15};
-  for (int i = 0; i < 3; ++i)
+  // 7, 9, 11, 13, 15 * 2^k: the whole odd factor in the last pass
+  const int odds[5] = {7, 9, 11, 13, 15};
+  for (int i = 0; i < 5; ++i)
     if (rem % odds[i] == 0 && fft_radix_ok(rem / odds[i])) return Radices{16, rem / odds[i], odds[i]};
   return Radices{0, 0, 0};
 }

@@ -1,6 +1,6 @@
 // Transform stages between spectral and physical space: host API, twiddle tables and the length
 // dispatch.  The kernels (x transforms, z physical stage, test C2C) are in fft_impl.hpp and are
-// instantiated per length family in fft_pow2.hip, fft_r3.hip and fft_r5.hip.
+// instantiated per length family in fft_pow2.hip and fft_r{3,5,7,9,11,13,15}.hip.
 #include "fft_impl.hpp"
 
 namespace channel {
@@ -55,7 +55,7 @@ void Twiddles::release() {
 }
 
 // transform lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280),
-// 7*2^k (112..1792), 9*2^k (144..1152), 15*2^k (240..1920)
+// 7*2^k (112..1792), 9*2^k (144..1152), 15*2^k (240..1920), 11*2^k (176..1408), 13*2^k (208..1664)
 #define CH_CASE_N(V, ...) \
   case V: { constexpr int NN = V; __VA_ARGS__; } break;
 #define CH_DISPATCH_N(N_, ...)                                                                              \
@@ -72,6 +72,9 @@ void Twiddles::release() {
     CH_CASE_N(144, __VA_ARGS__) CH_CASE_N(288, __VA_ARGS__) CH_CASE_N(576, __VA_ARGS__)                     \
     CH_CASE_N(1152, __VA_ARGS__) CH_CASE_N(240, __VA_ARGS__) CH_CASE_N(480, __VA_ARGS__)                    \
     CH_CASE_N(960, __VA_ARGS__) CH_CASE_N(1920, __VA_ARGS__)                                                \
+    CH_CASE_N(176, __VA_ARGS__) CH_CASE_N(352, __VA_ARGS__) CH_CASE_N(704, __VA_ARGS__)                     \
+    CH_CASE_N(1408, __VA_ARGS__) CH_CASE_N(208, __VA_ARGS__) CH_CASE_N(416, __VA_ARGS__)                    \
+    CH_CASE_N(832, __VA_ARGS__) CH_CASE_N(1664, __VA_ARGS__)                                                \
     default: CH_CHECK(false, "unsupported FFT length " << N_);                                              \
   }
 

@@ -1543,13 +1543,15 @@ void fft_test_len(void* data, int batch, int dir, const Twiddles& tw, bool fp64,
 }
 
 // the lengths with kernels: 2^k (16..2048), 3*2^k (48..1536), 5*2^k (80..1280), 7*2^k (112..1792),
-// 9*2^k (144..1152), 15*2^k (240..1920)
+// 9*2^k (144..1152), 15*2^k (240..1920), 11*2^k (176..1408), 13*2^k (208..1664)
 #define CH_FFT_POW2_LENGTHS(X) X(16) X(32) X(64) X(128) X(256) X(512) X(1024) X(2048)
 #define CH_FFT_R3_LENGTHS(X) X(48) X(96) X(192) X(384) X(768) X(1536)
 #define CH_FFT_R5_LENGTHS(X) X(80) X(160) X(320) X(640) X(1280)
 #define CH_FFT_R7_LENGTHS(X) X(112) X(224) X(448) X(896) X(1792)
 #define CH_FFT_R9_LENGTHS(X) X(144) X(288) X(576) X(1152)
 #define CH_FFT_R15_LENGTHS(X) X(240) X(480) X(960) X(1920)
+#define CH_FFT_R11_LENGTHS(X) X(176) X(352) X(704) X(1408)
+#define CH_FFT_R13_LENGTHS(X) X(208) X(416) X(832) X(1664)
 #define CH_FFT_INSTANTIATE(NN)                                                                              \
   template void fft_xb_len<NN>(const XArgs&, const XSrc&, void*, const Twiddles&, bool, hipStream_t);      \
   template void fft_xf_len<NN>(const XArgs&, const void*, const XDst&, const Twiddles&, bool, hipStream_t); \
@@ -1567,5 +1569,7 @@ CH_FFT_R5_LENGTHS(CH_FFT_EXTERN_ALL)
 CH_FFT_R7_LENGTHS(CH_FFT_EXTERN_ALL)
 CH_FFT_R9_LENGTHS(CH_FFT_EXTERN_ALL)
 CH_FFT_R15_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R11_LENGTHS(CH_FFT_EXTERN_ALL)
+CH_FFT_R13_LENGTHS(CH_FFT_EXTERN_ALL)
 
 }  // namespace channel

@@ -437,7 +437,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   // when the substep uses the previous nonlinear term); input i goes to slot i % NS and is
   // prefetched when input i - NS is committed
   constexpr int D = kGldsTile ? 1 : NS;  // (one spare tile: one field ahead)
-  static_assert(D >= 1 && D <= 3, "prefetch distance: the first D inputs of a tile are issued explicitly");
+  static_assert(D >= 1 && D <= 7, "prefetch distance: the first D inputs of a tile are issued explicitly");
   const int nin = zprev ? 7 : 5;
   auto src_of = [&](int i) -> const T2* {
     switch (i) {
@@ -456,10 +456,18 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       if (I < nin) st.template prefetch_at<I % NS>(src_of(I), l0);
     }
   };
+  // the first D inputs of the tile starting at line l0
+  auto ahead_first = [&](int l0) {
+    ahead(std::integral_constant<int, 0>{}, l0);
+    if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, l0);
+    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, l0);
+    if constexpr (D > 3) ahead(std::integral_constant<int, 3>{}, l0);
+    if constexpr (D > 4) ahead(std::integral_constant<int, 4>{}, l0);
+    if constexpr (D > 5) ahead(std::integral_constant<int, 5>{}, l0);
+    if constexpr (D > 6) ahead(std::integral_constant<int, 6>{}, l0);
+  };
   if (a.mode == 1 && lb < ntiles) {
-    ahead(std::integral_constant<int, 0>{}, lb * W);
-    if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, lb * W);
-    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, lb * W);
+    ahead_first(lb * W);
   }
   // optional per-phase shader-clock accounting (CHANNEL_KSPEC_PROF)
   const bool prof_on = a.prof != nullptr;
@@ -799,9 +807,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
       if (!kGldsTile && has_next) {
-        ahead(std::integral_constant<int, 0>{}, next_line0);
-        if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
-    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
+        ahead_first(next_line0);
       }
     } else {
       // ---------------- prepare only: fields from the state --------------------------------
@@ -848,9 +854,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       }
       KSPEC_STAMP(9)
       if (kGldsTile && has_next) {
-        ahead(std::integral_constant<int, 0>{}, next_line0);
-        if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
-        if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
+        ahead_first(next_line0);
       }
       continue;
     }
@@ -957,9 +961,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     }
     KSPEC_STAMP(9)
     if (kGldsTile && has_next) {
-      ahead(std::integral_constant<int, 0>{}, next_line0);
-      if constexpr (D > 1) ahead(std::integral_constant<int, 1>{}, next_line0);
-    if constexpr (D > 2) ahead(std::integral_constant<int, 2>{}, next_line0);
+      ahead_first(next_line0);
     }
   }  // tile loop
 #undef KSPEC_STAMP
@@ -1203,14 +1205,15 @@ static bool kspec_w8() {
   return on;
 }
 
-// CHANNEL_KSPEC_VAR = w4 | ns2 (A/B at R = 3, the small grids): 4 lines per block instead of 8,
-// or two register prefetch slots instead of one
+// CHANNEL_KSPEC_VAR = w4 | ns2 | ns5 | ns7 (A/B at R = 3, the small grids): 4 lines per block
+// instead of 8, or 2 / 5 / 7 register prefetch slots (5 and 7: every input of a tile issued at
+// its start, one exposed memory latency instead of one per prefetch window)
 static int kspec_var_env() {
   static const int v = [] {
     const char* e = std::getenv("CHANNEL_KSPEC_VAR");
     if (!e) return 0;
     const std::string s(e);
-    return s == "w4" ? 1 : (s == "ns2" ? 2 : 0);
+    return s == "w4" ? 1 : (s == "ns2" ? 2 : (s == "ns7" ? 3 : (s == "ns5" ? 4 : 0)));
   }();
   return v;
 }
@@ -1220,7 +1223,10 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   if constexpr (R == 3 && PAR == 0) {
     if (const int v = kspec_var_env()) {
       constexpr int W3 = 4;
-      auto k = v == 1 ? kspec_kernel<3, T, W3, 1, kspec_xmode<3, T>(), 0> : kspec_kernel<3, T, 8, 2, kspec_xmode<3, T>(), 0>;
+      auto k = v == 1   ? kspec_kernel<3, T, W3, 1, kspec_xmode<3, T>(), 0>
+               : v == 3 ? kspec_kernel<3, T, 8, 7, kspec_xmode<3, T>(), 0>
+               : v == 4 ? kspec_kernel<3, T, 8, 5, kspec_xmode<3, T>(), 0>
+                        : kspec_kernel<3, T, 8, 2, kspec_xmode<3, T>(), 0>;
       const int w = v == 1 ? W3 : 8;
       const int nt = (a.lines + w - 1) / w;
       dim3 grid(std::min(nt, resident_blocks(reinterpret_cast<const void*>(k), w * 64))), block(w * 64);

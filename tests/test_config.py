@@ -64,8 +64,8 @@ def test_file_and_example(native):
     assert c.NX == 128 and c.nsteps == 100 and c.out_G == "G.h5"
 
 
-@pytest.mark.parametrize("bad", ["NX = 100; NY = 33; NZ = 17;",      # NX not m*2^k (m = 1, 3, 5, 7, 9, 15)
-                                 "NX = 176; NY = 33; NZ = 17;",      # 11*2^k
+@pytest.mark.parametrize("bad", ["NX = 100; NY = 33; NZ = 17;",      # NX not m*2^k (m = 1, 3, ..., 15)
+                                 "NX = 272; NY = 33; NZ = 17;",      # 17*2^k
                                  "NX = 2304; NY = 33; NZ = 17;",     # 9*2^k above 2048
                                  "NX = 64; NY = 33; NZ = 16;",       # 2NZ-2 = 30 likewise
                                  "NX = 24; NY = 33; NZ = 17;",       # 3*2^k below 48
@@ -81,9 +81,9 @@ def test_invalid(native, bad):
 
 @pytest.mark.parametrize("nx,nz", [(96, 97), (192, 49), (384, 193), (768, 385), (1536, 769), (80, 81), (1280, 641),
                                    (48, 25), (2048, 1025), (112, 73), (1792, 481), (576, 289), (1152, 577),
-                                   (960, 121), (1920, 961)])
+                                   (960, 121), (1920, 961), (176, 89), (1408, 705), (208, 105), (1664, 833)])
 def test_non_power_of_two_lengths(native, nx, nz):
-    """Grids of the form m*2^k, m = 3, 5, 7, 9, 15 (cuFFT plans of any length in the reference,
+    """Grids of the form m*2^k, m = 3, 5, 7, 9, 11, 13, 15 (cuFFT plans of any length in the reference,
     fft.c:17-23)."""
     c = native.Config.from_string(f"NX = {nx}; NY = 33; NZ = {nz};")
     assert c.NX == nx and c.NZ == nz

@@ -82,10 +82,11 @@ def test_d1_dense_mfma(native, NY):
 
 @pytest.mark.parametrize("n", [16, 32, 64, 128, 256, 512, 1024, 2048,
                                48, 96, 192, 384, 768, 1536, 80, 160, 320, 640, 1280,
-                               112, 224, 448, 896, 1792, 144, 288, 576, 1152, 240, 480, 960, 1920])
+                               112, 224, 448, 896, 1792, 144, 288, 576, 1152, 240, 480, 960, 1920,
+                               176, 352, 704, 1408, 208, 416, 832, 1664])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_fft_c2c(native, n, dtype):
-    """Batched C2C against numpy, powers of two and the radix-3/5/7/9/15 plans (m*2^k)."""
+    """Batched C2C against numpy, powers of two and the radix-3/5/7/9/11/13/15 plans (m*2^k)."""
     rng = np.random.default_rng(n)
     x = rng.standard_normal((7, n)) + 1j * rng.standard_normal((7, n))
     xt = torch.tensor(x, dtype=dtype, device=DEV)
@@ -99,7 +100,7 @@ def test_fft_c2c(native, n, dtype):
 @pytest.mark.parametrize("NX,nkz", [(32, 11), (128, 43), (1024, 20), (2048, 9),
                                     (96, 13), (192, 11), (384, 20), (768, 9), (1536, 5), (80, 7), (1280, 6),
                                     (112, 9), (448, 13), (1792, 5), (144, 7), (1152, 6), (240, 11), (960, 7),
-                                    (1920, 5)])
+                                    (1920, 5), (176, 9), (1408, 5), (208, 7), (1664, 5)])
 @pytest.mark.parametrize("dtype", [torch.complex64, torch.complex128])
 def test_xfft(native, NX, nkz, dtype):
     rng = np.random.default_rng(NX)
@@ -191,6 +192,8 @@ def test_xfft_blocked_layout(native, NX, nkz, dtype, nt, variant):
                                           (8, 144, torch.complex64), (4, 1152, torch.complex128),
                                           (8, 240, torch.complex128), (4, 960, torch.complex64),
                                           (2, 1920, torch.complex64), (2, 1920, torch.complex128),
+                                          (8, 176, torch.complex128), (2, 1408, torch.complex64),
+                                          (8, 208, torch.complex64), (2, 1664, torch.complex128),
                                           (1024, 1024, torch.complex64), (1024, 1024, torch.complex128),
                                           (512, 2048, torch.complex64)])
 def test_zphys(native, NX, Nzp, dtype):

@@ -22,10 +22,11 @@ def make_solver(native, **kw):
 
 
 @pytest.mark.parametrize("NX,NY,NZ", [(32, 33, 17), (32, 65, 33), (96, 97, 97), (48, 33, 41), (112, 33, 73),
-                                      (240, 33, 57)])
+                                      (240, 33, 57), (176, 33, 105)])
 def test_gpu_matches_oracle_fp64(native, NX, NY, NZ):
     """(96, 97, 97): NX = 96 and 2NZ-2 = 192 run the radix-3 transform plans; (48, 33, 41): 48 and 80;
-    (112, 33, 73): 7*2^k and 9*2^k (2NZ-2 = 144); (240, 33, 57): 15*2^k and 7*2^k (112).
+    (112, 33, 73): 7*2^k and 9*2^k (2NZ-2 = 144); (240, 33, 57): 15*2^k and 7*2^k (112);
+    (176, 33, 105): 11*2^k and 13*2^k (208).
     The fixed step shrinks with the grid so the random state stays within the CFL limit."""
     dt = 0.01 * min(1.0, 32.0 / NX)
     kw = dict(NX=NX, NY=NY, NZ=NZ, Re=400.0, precision="fp64", dt_fixed=dt, stats_every=0, log_every=0,
