@@ -749,8 +749,11 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   // (fft1024_4x16x16: pad one slot per 64 elements, its own twiddle tables after the half plan's)
   // ZF = 3: the same plan, and H_z through it as a complex transform of (Hz, 0) (its outputs k < nkz
   // are the spectrum directly: no mirror, no half-length plan, one LDS round trip)
+  // ZF = 4: the same, with the H_z of two consecutive rows of the wave transformed together as
+  // (Hz_a + i Hz_b) and split like Hx / Hy (one 1024-point transform per two rows instead of two)
   constexpr bool kR4 = kRegEdge && sizeof(T) == 4 && NZP == 1024 && ZF >= 2;
-  constexpr bool kR4Hz = kR4 && ZF == 3;
+  constexpr bool kR4Hz = kR4 && ZF >= 3;
+  constexpr bool kPairHz = kR4 && ZF == 4;
   constexpr int PITCH = kR4 ? 1040 : (SH == 5 ? NZP + NZP / 32 : FftPitch<NZP>::value);
   constexpr int TPR = TPRT;  // threads per row
   constexpr int NWB = ZWT * TPR / 64;     // waves per block
@@ -863,6 +866,29 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   if constexpr (kPrefetch) {
     if (g < ngroups) fetch(g * ZWT + w, 0, pa, pb);
   }
+  // kPairHz: H_z of the wave's previous row, waiting for its partner (wave-uniform state), parked
+  // in a per-wave LDS area (slot pair i / 2 of lane l at (i / 2) * 64 + l: conflict-free b64
+  // accesses) instead of 16 registers held across the next row's inverse transforms
+  __shared__ T2 hzbuf[kPairHz ? ZWT * EP / 2 * 64 : 1];
+  long long rprev = 0;
+  bool held = false;
+  const T scz = static_cast<T>(0.5 * a.scale);
+  // H_z^(k) of rows ra (the real part of the packed row) and rb (the imaginary part) from the
+  // transform zh of (Hz_ra + i Hz_rb); rb < 0: a single row, zh the transform of (Hz_ra, 0)
+  auto hz_split_store = [&](T2 (&zh)[EP], long long ra, long long rb, int tt) {
+    const int src = (64 - tt) & 63;
+#pragma unroll
+    for (int i = 0; i < MK; ++i) {
+      const int k = tt + TPR * i;
+      const T2 pm{__shfl(zh[15 - i].x, src), __shfl(zh[15 - i].y, src)};
+      const T2 Zm = tt != 0 ? pm : zh[(16 - i) & 15];
+      if (k < nkz) {
+        const T2 Z = zh[i];
+        zstore(2, zaddr(ra, k), T2{(Z.x + Zm.x) * scz, (Z.y - Zm.y) * scz});
+        if (rb >= 0) zstore(2, zaddr(rb, k), T2{(Z.y + Zm.y) * scz, -(Z.x - Zm.x) * scz});
+      }
+    }
+  };
   // Rows past the end (TPR < 64 only: the host checks nrows % ZWT == 0 otherwise) run the
   // transforms on zeros and skip every global access.  The loop is block-uniform.
   for (; g < ngroups; g += gridDim.x) {
@@ -1061,7 +1087,26 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
       if (more) fetch(rnext, 0, pa, pb);
     }
     row_sync<TPRF>();
-    if constexpr (kR4Hz) {
+    if constexpr (kPairHz) {
+      T2* hb = hzbuf + w * (EP / 2) * 64 + t;
+      if (!held) {
+#pragma unroll
+        for (int i = 0; i < EP / 2; ++i) hb[i * 64] = T2{hz[2 * i], hz[2 * i + 1]};
+        rprev = r;
+        held = true;
+      } else {
+        T2 zh[EP];
+#pragma unroll
+        for (int i = 0; i < EP / 2; ++i) {
+          const T2 hp = hb[i * 64];
+          zh[2 * i] = T2{hp.x, hz[2 * i]};
+          zh[2 * i + 1] = T2{hp.y, hz[2 * i + 1]};
+        }
+        if (!(a.diag & 1)) fft1024_4x16x16<false>(zh, row, twm, tw3, t);
+        hz_split_store(zh, rprev, r, t);
+        held = false;
+      }
+    } else if constexpr (kR4Hz) {
       T2 zh[EP];
 #pragma unroll
       for (int i = 0; i < EP; ++i) zh[i] = T2{hz[i], T(0)};
@@ -1131,6 +1176,25 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
     }
     }
     row_sync<TPRF>();  // this row's last LDS reads precede the next row's writes
+  }
+  if constexpr (kPairHz) {
+    // an odd count of rows: the last one's H_z alone (the (Hz, 0) transform, split as a pair)
+    if (held) {
+      int tl = threadIdx.x;
+      asm volatile("" : "+v"(tl));
+      t = tl % TPR;
+      row = s + (tl / TPR) * PITCH;
+      const T2* hb = hzbuf + (tl / TPR) * (EP / 2) * 64 + t;
+      T2 zh[EP];
+#pragma unroll
+      for (int i = 0; i < EP / 2; ++i) {
+        const T2 hp = hb[i * 64];
+        zh[2 * i] = T2{hp.x, T(0)};
+        zh[2 * i + 1] = T2{hp.y, T(0)};
+      }
+      if (!(a.diag & 1)) fft1024_4x16x16<false>(zh, row, twm, tw3, t);
+      hz_split_store(zh, rprev, -1, t);
+    }
   }
   // block maxima -> one atomicMax per block and quantity
   for (int o = 32; o >= 1; o >>= 1) {
@@ -1397,7 +1461,7 @@ inline bool zreg_enabled() {
   return on;
 }
 
-// CHANNEL_ZFFT = 0 | 1 | 2 | 3: the 1024-point fp32 z-stage row transforms (zphys_kernel ZF, A/B).
+// CHANNEL_ZFFT = 0 | 1 | 2 | 3 | 4: the 1024-point fp32 z-stage row transforms (zphys_kernel ZF, A/B).
 // Default 3 (4 x 16 x 16 for all five transforms of a row); measured per 8-plane chunk alone at
 // 1024x385x1024: 60.9 / 58.5 / 57.9 / 56.9 us, bench 33.13 (ZF 1) / 32.97 / 32.79 ms/step
 // (gpurun_out/g10_*, profiles/r05/zfft_ab.txt)
@@ -1442,6 +1506,7 @@ static void zphys_launch_tpr(const ZArgs& a, void* fields, const Twiddles& tw, h
     if (!seg && zh && zf == 0) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 0>;
     if (!seg && zh && zf == 1) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 1>;
     if (!seg && zh && zf == 2) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 2>;
+    if (!seg && zh && zf == 4) kern = zphys_kernel<NN, T, false, true, TPR, ZR, WPE, 4>;
   }
   const long long ngroups = (nrows + ZR - 1) / ZR;
   const long long cap = zpers_enabled() ? persist_blocks(reinterpret_cast<const void*>(kern), ZR * TPR, "CHANNEL_Z_BPC") : ngroups;

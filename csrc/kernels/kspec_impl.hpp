@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   __shared__ double xs_mem[kspec_scratch_doubles<R, W, H>()];
   __shared__ double lx_buf[H == 2 ? W * 4 * LineG<2>::kXK : 1];
   __shared__ int lx_flag[H == 2 ? W * 2 : 1];
-  const int lane = __lane_id();
+  int lane = __lane_id();  // (re-laundered per tile in the LEAN variant: see the tile loop)
   const int wv = threadIdx.x / 64;
   const int w = wv % W;   // line slot of the tile
   const int hh = wv / W;  // half of the line (H = 2)
@@ -479,6 +479,10 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     tprev = now_;                                                 \
   }
   for (int tile = lb; tile < ntiles; tile += gridDim.x) {
+    // the per-row masks and offsets derived from the lane (row < N, j == 0, ...) are loop
+    // invariants; hoisted out of the tile loop they stay live across every phase (at the
+    // 256-register cap of two waves per SIMD they were spilled)
+    if constexpr (LEAN) asm volatile("" : "+v"(lane));
     const int line0 = tile * W;
     st.set_line0(line0);
     const int line = line0 + w;
