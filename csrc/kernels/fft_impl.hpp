@@ -82,6 +82,16 @@ static bool xplanes_enabled() {
   return on;
 }
 
+// CHANNEL_XSEGROWS=0: the per-element segment lookups of the exchange-segment x kernels (A/B of
+// the per-thread row table, kSegRows)
+static bool xsegrows_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CHANNEL_XSEGROWS");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
 static bool xwide_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CHANNEL_XWIDE");
@@ -121,8 +131,36 @@ __device__ __forceinline__ SegPos seg_find_win(const int* start, const long long
   return i >= b.start ? b : a;
 }
 // kx segment addressing of the x kernels: kSegOne = one block, no self block (one rank);
-// kSegWin = window lookup (seg_find_win); kSegFull = per-element lookup
-constexpr int kSegOne = 0, kSegWin = 1, kSegFull = 2;
+// kSegWin = window lookup (seg_find_win); kSegFull = per-element lookup; kSegRows = per-thread row
+// table: a thread's kx rows are the same in every tile, so their segments are looked up once per
+// launch (SegRows) and a tile's access is one 32-bit multiply-add per element (the per-element
+// lookups of the other modes spilled 375-402 SGPRs into VGPR lanes at 1024 points)
+constexpr int kSegOne = 0, kSegWin = 1, kSegFull = 2, kSegRows = 3;
+constexpr int kSegRowsMax = 24;  // rows per thread with a table (longer rows keep the lookups)
+// kSegRows: element offset of row i at y = 0 (off + (i - start) nkz), the y stride of its segment
+// (count nkz), and whether the segment is a self block, for the K rows i = (tid + k NT) / CW of a
+// thread (clamped to the last row like the accesses)
+template <int K>
+struct SegRows {
+  unsigned a[K], b[K];
+  unsigned self = 0;
+  template <int NT, int CW, int NROW>
+  __device__ __forceinline__ void build(const int* start, const long long* off, int n, int self_seg, int nself, int nkz,
+                                        int tid) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = min((tid + k * NT) / CW, NROW - 1);
+      const SegPos sp = seg_find<kMaxSeg>(start, off, n, i);
+      a[k] = static_cast<unsigned>(sp.off) + static_cast<unsigned>(i - sp.start) * static_cast<unsigned>(nkz);
+      b[k] = static_cast<unsigned>(sp.count) * static_cast<unsigned>(nkz);
+      if (static_cast<unsigned>(sp.idx - self_seg) < static_cast<unsigned>(nself)) self |= 1u << k;
+    }
+  }
+  __device__ __forceinline__ unsigned at(int k, int y, int kz) const {
+    return a[k] + static_cast<unsigned>(y) * b[k] + static_cast<unsigned>(kz);
+  }
+  __device__ __forceinline__ bool is_self(int k) const { return (self >> k) & 1u; }
+};
 template <int NT, int C>
 inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
   if (n == 1 && self_seg < 0 && off0 == 0) return kSegOne;
@@ -250,6 +288,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int nload = NKX * CW;
   CV v[EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
+  static_assert(SM != kSegRows || (NT % CW == 0 && EPT <= kSegRowsMax), "row table: a thread's rows repeat per access");
+  SegRows<SM == kSegRows ? EPT : 1> rt;
+  if constexpr (SM == kSegRows)
+    rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, a.nkz, tid);
   // tile t -> (f, y0, kz0); at each iteration the blocks of one XCD take consecutive tiles
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
@@ -311,6 +353,8 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
                               (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
                                   static_cast<unsigned>(sizeof(T2)));
         v[q] = a.nt ? ld_nt(r) : r;
+      } else if constexpr (SM == kSegRows) {
+        v[q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, y, kz));
       } else {
         const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                         : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
@@ -418,6 +462,11 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int tid = threadIdx.x;
   CV v[EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one destination block");
+  constexpr int KE = (NKX * CW + NT - 1) / NT;  // store passes over the retained kx rows
+  static_assert(SM != kSegRows || (NT % CW == 0 && KE <= kSegRowsMax), "row table: a thread's rows repeat per pass");
+  SegRows<SM == kSegRows ? KE : 1> rt;
+  if constexpr (SM == kSegRows)
+    rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, a.nkz, tid);
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
       y = (t % nyt) * YP;
@@ -505,6 +554,22 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     // this rank's own block goes straight into its spectral field (no self exchange)
     T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
+    if constexpr (SM == kSegRows) {
+#pragma unroll
+      for (int k = 0; k < KE; ++k) {
+        const int e = k * NT + tid;
+        const int i = e / CW, c = (e - i * CW) * V;
+        const int kz = kz0 + c % KC, yy = y + c / KC;
+        if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
+          const int x = i <= KXH ? i : NX - (NKX - i);
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, y, kz)) = w;
+        }
+      }
+      continue;
+    }
     for (int e0 = 0; e0 < NKX * CW; e0 += NT) {
       const int e = e0 + tid;
       const int i = e / CW, c = (e - i * CW) * V;
@@ -582,14 +647,19 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0),
            "xfft_backward: the blocked spectral layout needs one source block");
   constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;  // blocked layout: plane tiles when wide
+  // (row tables where a thread has at most kSegRowsMax rows: 2 VGPRs per row)
+  constexpr int kRowsK = ((2 * (NN / 3) + 1) * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
+  constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % (Cfg::C / V) == 0) ? kSegRows : kSegFull;
+  const bool rows = SMR == kSegRows && xsegrows_enabled();
   auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
               : a.npseg > 1   ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
+              : rows          ? xfft_backward_kernel<NN, T, false, WIDE, SMR, V>
                               : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : kSegFull) : (sm == kSegOne ? kSegOne : kSegFull), V,
+                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : kSegFull) : (sm == kSegOne ? kSegOne : (rows ? kSegRows : kSegFull)), V,
                     a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
@@ -606,15 +676,19 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
   CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0),
            "xfft_forward: the blocked spectral layout needs one destination block");
   constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;
+  constexpr int kRowsK = ((2 * (NN / 3) + 1) * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
+  constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % (Cfg::C / V) == 0) ? kSegRows : kSegFull;
+  const bool rows = SMR == kSegRows && xsegrows_enabled();
   auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
               : a.npseg > 1           ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
               : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
+              : rows          ? xfft_forward_kernel<NN, T, false, WIDE, SMR, V>
               : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
                               : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   xfft_note_variant("xfft_forward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb ? kSegOne : (a.npseg > 1 ? kSegFull : sm), V, a.kzb ? SLB : 0);
+                    a.kzb ? kSegOne : (a.npseg > 1 ? kSegFull : (sm != kSegOne && rows ? kSegRows : sm)), V, a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));
