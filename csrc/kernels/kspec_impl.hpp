@@ -197,14 +197,16 @@ struct Stage {
       return;
     }
     const int y0 = copy_row(), l = threadIdx.x % W;
+    T2* const tb = tile + row_off(y0) + l;  // (G = 0: row q at a compile-time LDS offset from it)
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int y = y0 + RPB * q;
       if (y < N) {
+        T2& dstl = G ? tile[row_off(y) + l] : tb[RPB * q * PITCH];
         if constexpr (kRegSlots) {
-          tile[row_off(y) + l] = pend[S][q];
+          dstl = pend[S][q];
         } else {
-          tile[row_off(y) + l] = dsrc[S][doff[S] + static_cast<unsigned>(RPB * q) * rs];
+          dstl = dsrc[S][doff[S] + static_cast<unsigned>(RPB * q) * rs];
         }
       }
     }
@@ -240,11 +242,12 @@ struct Stage {
     }
     lds_barrier();
     const int y0 = copy_row(), l = threadIdx.x % W;
+    const T2* const tb = tile + row_off(y0) + l;  // (G = 0: row q at a compile-time LDS offset from it)
     if (line0 + l < lines) {
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         const int y = y0 + RPB * q;
-        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * rs] = tile[row_off(y) + l];
+        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * rs] = G ? tile[row_off(y) + l] : tb[RPB * q * PITCH];
       }
     }
   }
