@@ -144,13 +144,13 @@ template <int K>
 struct SegRows {
   unsigned a[K], b[K];
   unsigned self = 0;
-  template <int NT, int CW, int NROW>
+  template <int NT, int CW, int NROW, int MAXS = kMaxSeg>
   __device__ __forceinline__ void build(const int* start, const long long* off, int n, int self_seg, int nself, int nkz,
                                         int tid) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int i = min((tid + k * NT) / CW, NROW - 1);
-      const SegPos sp = seg_find<kMaxSeg>(start, off, n, i);
+      const SegPos sp = seg_find<MAXS>(start, off, n, i);
       a[k] = static_cast<unsigned>(sp.off) + static_cast<unsigned>(i - sp.start) * static_cast<unsigned>(nkz);
       b[k] = static_cast<unsigned>(sp.count) * static_cast<unsigned>(nkz);
       if (static_cast<unsigned>(sp.idx - self_seg) < static_cast<unsigned>(nself)) self |= 1u << k;
@@ -292,6 +292,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   SegRows<SM == kSegRows ? EPT : 1> rt;
   if constexpr (SM == kSegRows)
     rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, a.nkz, tid);
+  // SEG (pencil: the x-expanded output blocked by x range) with row tables: the thread's x rows
+  // x = (tid + k NT) / CW of the store passes, looked up once like the kx rows
+  constexpr int KXS = (NX * CW + NT - 1) / NT;
+  constexpr bool kXRows = SEG && SM == kSegRows;
+  static_assert(!kXRows || KXS <= kSegRowsMax, "x row table too long");
+  SegRows<kXRows ? KXS : 1> xt;
+  if constexpr (kXRows) xt.template build<NT, CW, NX, 8>(a.x_start, a.poff, a.npseg, -1, 0, a.nkz, tid);
   // tile t -> (f, y0, kz0); at each iteration the blocks of one XCD take consecutive tiles
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
@@ -414,6 +421,21 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     T2* out = phys + f * a.field_stride_phys;
+    if constexpr (kXRows) {
+#pragma unroll
+      for (int k = 0; k < KXS; ++k) {
+        const int e = tid + k * NT;
+        const int x = e / CW, c = (e - x * CW) * V;
+        const int kz = kz0 + c % KC, yy = y + c / KC;
+        if (e < NX * CW && kz < a.nkz && yy < a.ny) {
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>(out + xt.at(k, yy, kz)) = w;
+        }
+      }
+      continue;
+    }
     for (int e = tid; e < NX * CW; e += NT) {
       const int x = e / CW, c = (e - x * CW) * V;
       const int kz = kz0 + c % KC, yy = y + c / KC;
@@ -467,6 +489,12 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   SegRows<SM == kSegRows ? KE : 1> rt;
   if constexpr (SM == kSegRows)
     rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, a.nkz, tid);
+  // SEG (pencil: the x-expanded input blocked by x range) with row tables: the thread's x rows of
+  // the fetch (x = (tid + q NT) / CW, clamped), looked up once
+  constexpr bool kXRows = SEG && SM == kSegRows;
+  static_assert(!kXRows || (EPT <= kSegRowsMax && !QM::on), "x row table too long");
+  SegRows<kXRows ? EPT : 1> xt;
+  if constexpr (kXRows) xt.template build<NT, CW, NX, 8>(a.x_start, a.poff, a.npseg, -1, 0, a.nkz, tid);
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
       y = (t % nyt) * YP;
@@ -490,7 +518,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       const int x = min(QM::on ? quad_row(tid) + q * (NT / CW) : e / CW, NX - 1);
       const int c = (QM::on ? quad_col(tid) : e % CW) * V;
       const int kz = min(kz0 + c % KC, a.nkz - V), yy = min(y + c / KC, a.ny - 1);
-      if constexpr (SEG) {
+      if constexpr (kXRows) {
+        v[q] = *reinterpret_cast<const CV*>(in + xt.at(q, yy, kz));
+      } else if constexpr (SEG) {
         const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
         v[q] = *reinterpret_cast<const CV*>(in + static_cast<unsigned>(sp.off) +
                                             static_cast<unsigned>(yy * sp.count + x - sp.start) * static_cast<unsigned>(a.nkz) +
@@ -651,15 +681,18 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   constexpr int kRowsK = ((2 * (NN / 3) + 1) * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
   constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % (Cfg::C / V) == 0) ? kSegRows : kSegFull;
   const bool rows = SMR == kSegRows && xsegrows_enabled();
+  constexpr int kXRowsK = (NN * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
+  constexpr int SMX = (SMR == kSegRows && kXRowsK <= kSegRowsMax) ? kSegRows : kSegFull;
   auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
-              : a.npseg > 1   ? xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>
+              : a.npseg > 1   ? (rows ? xfft_backward_kernel<NN, T, true, WIDE, SMX, V>
+                                      : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>)
               : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
               : rows          ? xfft_backward_kernel<NN, T, false, WIDE, SMR, V>
                               : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : kSegFull) : (sm == kSegOne ? kSegOne : (rows ? kSegRows : kSegFull)), V,
+                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : (rows ? SMX : kSegFull)) : (sm == kSegOne ? kSegOne : (rows ? kSegRows : kSegFull)), V,
                     a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
@@ -679,8 +712,11 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
   constexpr int kRowsK = ((2 * (NN / 3) + 1) * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
   constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % (Cfg::C / V) == 0) ? kSegRows : kSegFull;
   const bool rows = SMR == kSegRows && xsegrows_enabled();
+  constexpr int kXRowsK = (NN * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
+  constexpr int SMX = (SMR == kSegRows && kXRowsK <= kSegRowsMax) ? kSegRows : kSegFull;
   auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
-              : a.npseg > 1           ? xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>
+              : a.npseg > 1           ? (rows ? xfft_forward_kernel<NN, T, true, WIDE, SMX, V>
+                                              : xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>)
               : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
               : rows          ? xfft_forward_kernel<NN, T, false, WIDE, SMR, V>
               : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
@@ -688,7 +724,7 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
   const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
   xfft_note_variant("xfft_forward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb ? kSegOne : (a.npseg > 1 ? kSegFull : (sm != kSegOne && rows ? kSegRows : sm)), V, a.kzb ? SLB : 0);
+                    a.kzb ? kSegOne : (a.npseg > 1 ? (rows ? SMX : kSegFull) : (sm != kSegOne && rows ? kSegRows : sm)), V, a.kzb ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));
