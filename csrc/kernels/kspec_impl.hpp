@@ -231,6 +231,54 @@ struct Stage {
   }
   // rows >= N are written too: the operators keep them at exactly zero
   __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&x)[2][R]) { store(dst, x[0], x[1]); }
+  // Two fields stored through two given tiles behind ONE barrier (instead of one barrier per field).
+  // The caller picks tiles whose previous readers have all passed a barrier since (STORE2).
+  __device__ __forceinline__ void store2_into(T2* ta, T2* tb, T2* __restrict__ da, const double (&ra)[R],
+                                              const double (&ia)[R], T2* __restrict__ db, const double (&rb)[R],
+                                              const double (&ib)[R]) {
+    {
+      T2* ca = ta + row_off(h * 64 * R + lane * R) + w;
+      T2* cb = tb + row_off(h * 64 * R + lane * R) + w;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        ca[r * PITCH] = T2{static_cast<T>(ra[r]), static_cast<T>(ia[r])};
+        cb[r * PITCH] = T2{static_cast<T>(rb[r]), static_cast<T>(ib[r])};
+      }
+    }
+    lds_barrier();
+    const int y0 = copy_row(), l = threadIdx.x % W;
+    const T2* const pa = ta + row_off(y0) + l;
+    const T2* const pb = tb + row_off(y0) + l;
+    if (line0 + l < lines) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int y = y0 + RPB * q;
+        if (y < N) {
+          const unsigned o = toff + static_cast<unsigned>(RPB * q) * rs;
+          da[o] = G ? ta[row_off(y) + l] : pa[RPB * q * PITCH];
+          db[o] = G ? tb[row_off(y) + l] : pb[RPB * q * PITCH];
+        }
+      }
+    }
+  }
+  // one field through a given tile (same rule)
+  __device__ __forceinline__ void store_into(T2* t, T2* __restrict__ dst, const double (&re)[R], const double (&im)[R]) {
+    {
+      T2* c = t + row_off(h * 64 * R + lane * R) + w;
+#pragma unroll
+      for (int r = 0; r < R; ++r) c[r * PITCH] = T2{static_cast<T>(re[r]), static_cast<T>(im[r])};
+    }
+    lds_barrier();
+    const int y0 = copy_row(), l = threadIdx.x % W;
+    const T2* const tb = t + row_off(y0) + l;
+    if (line0 + l < lines) {
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int y = y0 + RPB * q;
+        if (y < N) dst[toff + static_cast<unsigned>(RPB * q) * rs] = G ? t[row_off(y) + l] : tb[RPB * q * PITCH];
+      }
+    }
+  }
   // (re, im) rows of a line, optionally scaled (wave-uniform)
   __device__ __forceinline__ void store(T2* __restrict__ dst, const double (&re)[R], const double (&im)[R],
                                         double sc = 1.0) {
@@ -300,6 +348,16 @@ constexpr bool kspec_double_tile() {
          158 * 1024;
 }
 
+// two extra store tiles (STORE2: paired output stores behind one barrier) where the LDS has room
+template <int R, typename T, int W, int H = 1>
+constexpr bool kspec_store2_tiles() {
+  return H == 1 && kspec_double_tile<R, T, W, H>() &&
+         (kspec_tables_in_lds<R, T, W, H>() ? kspec_lds_tables_doubles<R, T, W, H>() * 8 : 0) +
+                 4 * Stage<R, T, W, 1, false, H>::TILE * static_cast<int>(sizeof(typename Cplx<T>::type)) +
+                 kspec_scratch_doubles<R, W, H>() * 8 <=
+             158 * 1024;
+}
+
 // Reference-parity variants (compile-time, PAR bits): kParDD = explicit viscous D2 as D1 o D1
 // (RK3_kernels.cu:160-164, derivatives_nu_double.cu:440-446); kParAnalytic = analytic influence
 // functions (bilplacSolver_double.cu:56-250, l1/l2 typo fixed).  The default (PAR = 0) is the
@@ -336,7 +394,11 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   constexpr bool LEAN = H == 1 && W >= 8 && R >= 5;
   static_assert(H == 1 || (SPLIT == 0 && GLM == 0), "two-wave lines: the fused kernel");
   __shared__ double tab_lds[TLDS ? NTAB : 1];
-  __shared__ T2 tile_mem[(kDoubleTile ? 2 : 1) * St::TILE];
+  // STORE2: paired stores of the R fields and the outputs through two extra tiles (not with the
+  // async staging, which fills the spare tile during the output stores; not in the split kernel)
+  constexpr bool kStore2 = kspec_store2_tiles<R, T, W, H>() && !kGldsTile && SPLIT == 0;
+  constexpr int NTILES = kStore2 ? 4 : (kDoubleTile ? 2 : 1);
+  __shared__ T2 tile_mem[NTILES * St::TILE];
   __shared__ double xs_mem[kspec_scratch_doubles<R, W, H>()];
   __shared__ double lx_buf[H == 2 ? W * 4 * LineG<2>::kXK : 1];
   __shared__ int lx_flag[H == 2 ? W * 2 : 1];
@@ -412,7 +474,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     t.trap = tg.trap + z + thalf;  // (the mean line's weights: otherwise R 64-bit addresses live across the tile loop)
   };
   // zero tiles: rows >= N stay zero for the whole kernel (Stage::commit)
-  for (int i = threadIdx.x; i < (kDoubleTile ? 2 : 1) * St::TILE; i += NT) tile_mem[i] = T2{0, 0};
+  for (int i = threadIdx.x; i < NTILES * St::TILE; i += NT) tile_mem[i] = T2{0, 0};
   __syncthreads();
   const Xl<XM> xl{xs_mem + wv * XS};
   // statistics reduction [4][64 R] in the staging tiles: between the phi store and the output
@@ -427,6 +489,8 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   const int ntiles = (a.lines + W - 1) / W;
   const int lb = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   St st{tile_mem, kDoubleTile ? tile_mem + St::TILE : nullptr, N, a.lines, lb * W, w, lane};
+  T2* const xt0 = tile_mem + 2 * St::TILE;  // (STORE2 only)
+  T2* const xt1 = tile_mem + 3 * St::TILE;
   st.set_layout(a.kzb);
   st.h = hh;
   // global row of (lane, r) in this wave
@@ -616,8 +680,12 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       }
       KSPEC_STAMP(1)
       if (a.store_r) {  // (the last substep's R is never read: the next substep has zeta = 0)
-        st.store(Rphi, RPn);
-        st.store(Romega, RWn);
+        if constexpr (kStore2) {
+          st.store2_into(xt0, xt1, Rphi, RPn[0], RPn[1], Romega, RWn[0], RWn[1]);
+        } else {
+          st.store(Rphi, RPn);
+          st.store(Romega, RWn);
+        }
       }
       KSPEC_STAMP(2)
 
@@ -920,6 +988,35 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     auto ostore = [&](void* dst, const double (&re)[R], const double (&im)[R], double sc = 1.0) {
       st.store(static_cast<T2*>(dst), re, im, sc);
     };
+    if constexpr (kStore2) {
+      if (a.out[4] == a.omega) {
+        // v and u, then w and omega_x, behind one barrier each (tiles: the extra pair, then the
+        // staging pair, whose last readers (the phi store) passed the first pair's barrier), then
+        // omega_z through the extra tile of the first pair (its readers passed the second barrier)
+        double x[2][R], x2[2][R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
+        st.store2_into(xt0, xt1, static_cast<T2*>(a.out[1]), vo[0], vo[1], static_cast<T2*>(a.out[0]), x[0], x[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          vel_w(r, x[0][r], x[1][r]);
+          const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+          const double br = (be * DDr + al * dvo[2][r]) * inv_k2, bi = (be * DDi + al * dvo[3][r]) * inv_k2;
+          x2[0][r] = -bi + be * vo[1][r];
+          x2[1][r] = br - be * vo[0][r];
+        }
+        st.store2_into(st.tile, st.tile2, static_cast<T2*>(a.out[2]), x[0], x[1], static_cast<T2*>(a.out[3]), x2[0], x2[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+          const double ar = (al * DDr - be * dvo[2][r]) * inv_k2, ai = (al * DDi - be * dvo[3][r]) * inv_k2;
+          x[0][r] = -al * vo[1][r] + ai - mf * dvo[2][r];
+          x[1][r] = al * vo[0][r] - ar;
+        }
+        st.store_into(xt0, static_cast<T2*>(a.out[5]), x[0], x[1]);
+        goto outputs_done;
+      }
+    }
     ostore(a.out[1], vo[0], vo[1]);  // v
     // omega_y: when out[4] is the omega state itself (the solver's layout) it is already stored;
     // the x transform reads its mean line (U) as 0
@@ -952,6 +1049,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       }
       ostore(a.out[5], x[0], x[1]);
     }
+  outputs_done:
     if (a.mean_diag && is_mean) {
       const double d0 = line_row_value<R, XM>(dvo[2], 0, g, lane), dN = line_row_value<R, XM>(dvo[2], N - 1, g, lane);
 #pragma unroll
