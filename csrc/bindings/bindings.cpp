@@ -107,13 +107,29 @@ torch::Tensor fft_c2c(torch::Tensor x, int dir) {
 }
 
 // x-direction backward/forward transforms on a single-rank layout (tests)
-torch::Tensor xfft_b(torch::Tensor spec, int NX, int Kx) {
+// combine = 1: spec holds the five K-SPEC outputs (D1 v, v, D1 omega, omega, phi) and the six
+// physical-stage fields u, v, w, omega_x, omega_y, omega_z are formed per element (XArgs::combine;
+// ax, az = 2 pi / LX, 2 pi / LZ, kz0 = global kz of local kz 0)
+void set_combine(XArgs& a, XSrc& s, const char* base, long long fstride, size_t esz, int combine, double ax, double az,
+                 int kz0) {
+  a.combine = combine;
+  a.ax = ax;
+  a.az = az;
+  a.kz_glob0 = kz0;
+  if (combine) {
+    a.nfields = 6;
+    for (int j = 0; j < 5; ++j) s.fld[j] = base + static_cast<size_t>(j) * fstride * esz;
+  }
+}
+
+torch::Tensor xfft_b(torch::Tensor spec, int NX, int Kx, int combine, double ax, double az, int kz0) {
   check_dev_tensor(spec, "spec");
   const bool f64 = is_fp64_complex(spec);
   TORCH_CHECK(spec.dim() == 4, "spec must be [F, ny, nkx, nkz]");
   const int F = spec.size(0), ny = spec.size(1), nkx = spec.size(2), nkz = spec.size(3);
   TORCH_CHECK(nkx == 2 * Kx + 1, "nkx != 2Kx+1");
-  auto phys = torch::zeros({F, ny, NX, nkz}, spec.options());
+  TORCH_CHECK(!combine || F == 5, "combine mode: five input fields");
+  auto phys = torch::zeros({combine ? 6 : F, ny, NX, nkz}, spec.options());
   XArgs a;
   a.NX = NX; a.nkx = nkx; a.Kx = Kx; a.nkz = nkz; a.ny = ny; a.nfields = F;
   a.field_stride_spec = static_cast<long long>(ny) * nkx * nkz;
@@ -123,6 +139,7 @@ torch::Tensor xfft_b(torch::Tensor spec, int NX, int Kx) {
   s.nsrc = 1;
   s.kx_start[0] = 0;
   s.kx_start[1] = nkx;
+  set_combine(a, s, static_cast<const char*>(spec.data_ptr()), a.field_stride_spec, spec.element_size(), combine, ax, az, kz0);
   xfft_backward(a, s, phys.data_ptr(), twiddles(NX, f64), f64, cur_stream());
   return phys;
 }
@@ -152,14 +169,15 @@ torch::Tensor xfft_f(torch::Tensor phys, int Kx) {
 // non-temporal spectral accesses (nt) -- on planes y0 .. y0 + ny - 1 of F fields of `rows` planes.
 // specb: 1-D complex buffer of F * spec_rows(rows) * nkx * nkzs elements (nkzs = nkz rounded up to 8)
 torch::Tensor xfft_b_blocked(torch::Tensor specb, int F, int rows, int y0, int ny, int NX, int Kx, int nkz, int nt,
-                             int zero_mean_field) {
+                             int zero_mean_field, int combine, double ax, double az) {
   check_dev_tensor(specb, "specb");
   const bool f64 = is_fp64_complex(specb);
   const int nkx = 2 * Kx + 1, nkzs = (nkz + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock;
   const long long fstride = static_cast<long long>(spec_rows(kSpecKzBlock, rows)) * nkx * nkzs;
   TORCH_CHECK(specb.dim() == 1 && specb.numel() == F * fstride, "specb must hold F blocked fields");
   TORCH_CHECK(y0 >= 0 && ny > 0 && y0 + ny <= rows, "plane range outside the fields");
-  auto phys = torch::zeros({F, ny, NX, nkz}, specb.options());
+  TORCH_CHECK(!combine || F == 5, "combine mode: five input fields");
+  auto phys = torch::zeros({combine ? 6 : F, ny, NX, nkz}, specb.options());
   XArgs a;
   a.NX = NX; a.nkx = nkx; a.Kx = Kx; a.nkz = nkz; a.ny = ny; a.nfields = F;
   a.field_stride_spec = fstride;
@@ -171,6 +189,7 @@ torch::Tensor xfft_b_blocked(torch::Tensor specb, int F, int rows, int y0, int n
   s.nsrc = 1;
   s.kx_start[0] = 0;
   s.kx_start[1] = nkx;
+  set_combine(a, s, static_cast<const char*>(specb.data_ptr()), fstride, specb.element_size(), combine, ax, az, 0);
   xfft_backward(a, s, phys.data_ptr(), twiddles(NX, f64), f64, cur_stream());
   return phys;
 }
@@ -256,10 +275,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("d1_mfma", &YLineOps::d1_mfma, py::arg("x"));
 
   m.def("fft_c2c", &fft_c2c, "batched in-LDS C2C FFT along the last axis; dir=+1 inverse (unnormalised)");
-  m.def("xfft_backward", &xfft_b);
+  m.def("xfft_backward", &xfft_b, py::arg("spec"), py::arg("NX"), py::arg("Kx"), py::arg("combine") = 0,
+        py::arg("ax") = 1.0, py::arg("az") = 2.0, py::arg("kz0") = 0);
   m.def("xfft_forward", &xfft_f);
   m.def("xfft_backward_blocked", &xfft_b_blocked, py::arg("specb"), py::arg("F"), py::arg("rows"), py::arg("y0"),
-        py::arg("ny"), py::arg("NX"), py::arg("Kx"), py::arg("nkz"), py::arg("nt") = 0, py::arg("zero_mean_field") = -1);
+        py::arg("ny"), py::arg("NX"), py::arg("Kx"), py::arg("nkz"), py::arg("nt") = 0, py::arg("zero_mean_field") = -1,
+        py::arg("combine") = 0, py::arg("ax") = 1.0, py::arg("az") = 2.0);
   m.def("xfft_forward_blocked", &xfft_f_blocked, py::arg("phys"), py::arg("specb"), py::arg("rows"), py::arg("y0"),
         py::arg("Kx"), py::arg("nt") = 0);
   m.def("zphys", &zphys_op);

@@ -98,8 +98,12 @@ std::string tcp_broadcast(const ProcInfo& pi, const std::string& payload, int ti
         m.sin_addr = reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr;
         freeaddrinfo(res);
         // a hostname that resolves to a loopback alias on the master only (127.0.1.1 through
-        // /etc/hosts) would accept local peers and refuse remote ones: listen on every interface
-        const bool loop_alias = (ntohl(m.sin_addr.s_addr) >> 24) == 127 && addr != "127.0.0.1" && addr != "localhost";
+        // /etc/hosts) would accept local peers and refuse remote ones: listen on every interface --
+        // but only when the launcher does not say the job is single-node (no LOCAL_WORLD_SIZE);
+        // a single-node job keeps the loopback bind (the bootstrap has no authentication)
+        const bool single_node = ws && lws && std::atoi(ws) <= std::atoi(lws);
+        const bool loop_alias = !single_node && (ntohl(m.sin_addr.s_addr) >> 24) == 127 && addr != "127.0.0.1" &&
+                                addr != "localhost";
         if (loop_alias) {
           std::fprintf(stderr, "[channel] bootstrap: MASTER_ADDR %s resolves to a loopback address; listening on every interface\n",
                        addr.c_str());

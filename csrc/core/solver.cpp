@@ -378,6 +378,15 @@ void* Solver::field_ptr(int f) const {
   CH_CHECK(false, "bad field index " << f);
 }
 
+// Input j of the x-backward's combine mode (XArgs::combine): 0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi
+// -- what K-SPEC leaves for the physical-space stage; the backward exchange of P > 1 moves these
+// five fields (the forward one the three H fields)
+void* Solver::in_field(int j) const {
+  static const Field kIn[kBwdFields] = {OUT0, OUT1, OUT2, OMEGA, PHI};
+  CH_CHECK(j >= 0 && j < kBwdFields, "bad combine input " << j);
+  return field_ptr(kIn[j]);
+}
+
 int Solver::kb_gstart(int c, int b) const {
   return plan_.kx_split.start[c] + Split::balanced(plan_.kx_split.count[c], nkb_).start[b];
 }
@@ -764,7 +773,10 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.nkz = p.nkz;
   xa.ny = p.ny_loc;
   xa.field_stride_phys = static_cast<long long>(physn_);
-  xa.zero_mean_field = 4;  // omega_y's spectral source is the omega state (mean line = U)
+  // u, v, w, omega_x, omega_y, omega_z formed per element from the five K-SPEC outputs (combine)
+  xa.combine = 1;
+  xa.ax = p.ax;
+  xa.az = p.az;
   xa.kz_glob0 = p.kz0;
   xa.lds_poison = lds_poison_enabled() ? 1 : 0;
   xa.nt = xnt_;
@@ -810,6 +822,7 @@ void Solver::transforms(int n, bool /*stats*/) {
     src.nsrc = 1;
     src.kx_start[0] = 0;
     src.kx_start[1] = p.nkx;
+    for (int j = 0; j < kBwdFields; ++j) src.fld[j] = in_field(j);
     xa.nfields = 6;
     xa.field_stride_spec = static_cast<long long>(spec_);
     XDst dst;
@@ -844,6 +857,7 @@ void Solver::transforms(int n, bool /*stats*/) {
         if (kzb_) xc.spec_y0 = y0;
         XSrc sc = src;
         sc.base = static_cast<char*>(out_) + so;
+        for (int j = 0; j < kBwdFields; ++j) sc.fld[j] = static_cast<const char*>(src.fld[j]) + so;
         xc.nfields = 6;
         ev(1, false, cs);
         xfft_backward(xc, sc, ph, tw_x_, fp64_, cs);
@@ -905,7 +919,7 @@ void Solver::transforms(int n, bool /*stats*/) {
   }
   src.kx_start[Pc] = dst.kx_start[Pc] = p.nkx;
   xa.nkz = p.nkz_loc;
-  xa.nfields = 1;
+  xa.nfields = 6;
   xa.field_stride_spec = static_cast<long long>(xstride_);
   if (pen) {  // x-expanded output blocked by destination row (x range)
     xa.npseg = Pr;
@@ -927,23 +941,23 @@ void Solver::transforms(int n, bool /*stats*/) {
   auto fld = [&](void* base, size_t stride, int f) { return static_cast<char*>(base) + static_cast<size_t>(f) * stride * esz_; };
   HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
   HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
-  for (int f = 0; f < 6; ++f) {
+  for (int f = 0; f < kBwdFields; ++f) {
     ev(4, false, s_comm_);
-    a2a_spec(field_ptr(OUT0 + f), fld(xbuf_, xstride_, f), true);
+    a2a_spec(in_field(f), fld(xbuf_, xstride_, f), true);
     ev(4, true, s_comm_);
-    HIP_CHECK(hipEventRecord(ev_a2a_[f], s_comm_));
   }
+  HIP_CHECK(hipEventRecord(ev_a2a_[0], s_comm_));
+  HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_a2a_[0], 0));
   ev(1, false);
-  for (int f = 0; f < 6; ++f) {
-    HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_a2a_[f], 0));
+  {
     XSrc sf = src;
-    sf.base = fld(xbuf_, xstride_, f);
-    XArgs xf1 = xa;
-    xf1.zero_mean_field = f == 4 ? 0 : -1;  // one field per call
-    xfft_backward(xf1, sf, fld(phys_, physn_, f), tw_x_, fp64_, s_comp_);
-    if (pen) {  // ship field f's x-blocks to the row group while field f+1 is transformed
-      HIP_CHECK(hipEventRecord(ev_b_[f], s_comp_));
-      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_b_[f], 0));
+    for (int j = 0; j < kBwdFields; ++j) sf.fld[j] = fld(xbuf_, xstride_, j);
+    xfft_backward(xa, sf, phys_, tw_x_, fp64_, s_comp_);
+  }
+  if (pen) {  // ship the x-blocks of the six fields to the row group
+    HIP_CHECK(hipEventRecord(ev_b_[0], s_comp_));
+    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_b_[0], 0));
+    for (int f = 0; f < 6; ++f) {
       ev(4, false, s_comm_);
       a2a_rows(fld(phys_, physn_, f), fld(zbuf_, zstride_, f), true);
       ev(4, true, s_comm_);
@@ -980,6 +994,7 @@ void Solver::transforms(int n, bool /*stats*/) {
     }
   }
   ev(3, false);
+  xa.nfields = 1;  // (one field per forward call)
   for (int f = 0; f < 3; ++f) {
     if (pen) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_bb_[f], 0));
     XDst df = dst;
@@ -1024,7 +1039,7 @@ void Solver::a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bh
       o.soff.assign(P, 0);
       o.rcount.assign(P, 0);
       o.roff.assign(P, 0);
-      char* spec = static_cast<char*>(field_ptr(OUT0 + f));
+      char* spec = static_cast<char*>(to_phys ? in_field(f) : field_ptr(OUT0 + f));
       char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
       const size_t lines_b = static_cast<size_t>(kb_cnt_[b]) * p.nkz_loc;
       for (int c = 0; c < P; ++c) {
@@ -1096,6 +1111,11 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
     CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
   }
+  // combine inputs: received blocks in the exchange buffer (five fields), own blocks in place
+  for (int j = 0; j < kBwdFields; ++j) {
+    src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
+    if (self_direct_) src.self_fld[j] = in_field(j);
+  }
 
   roctxRangePushA("xzx_slab_chunked");
   // K-SPEC / exchange overlap: blocks 0 .. NB-2 of the previous substep's K-SPEC go out whole as
@@ -1113,7 +1133,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
       ev(4, false, s_comm_);
-      a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+      a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
       ev(4, true, s_comm_);
     }
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
@@ -1123,7 +1143,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   }
   auto backward = [&](int k) {
     ev(4, false, s_comm_);
-    a2a_slab_rows(k * ch, ch, true, 6, bchunk, NB);
+    a2a_slab_rows(k * ch, ch, true, kBwdFields, bchunk, NB);
     ev(4, true, s_comm_);
     HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
   };
@@ -1135,10 +1155,15 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   // binds torch's bundled HIP 7.0 runtime and RCCL (same sonames), and there a captured step with the
   // second compute stream forked next to the RCCL exchanges segfaults in the runtime; eager steps and
   // /opt/rocm's 7.2 runtime -- bench.py and the drivers are torch-free -- capture it fine)
+  // (CHANNEL_PSTREAMS_CAPTURE=1 lifts the runtime-version gate: diagnosis of the 7.0 crash)
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
   if (s_comp2_) HIP_CHECK(hipStreamIsCapturing(s_comp_, &cst));
+  static const bool cap_force = [] {
+    const char* e = std::getenv("CHANNEL_PSTREAMS_CAPTURE");
+    return e && std::atoi(e) == 1;
+  }();
   const bool two = s_comp2_ != nullptr && !phase_timing_ && nch > 1 &&
-                   (cst == hipStreamCaptureStatusNone || hip_runtime_version() >= 70200000);
+                   (cst == hipStreamCaptureStatusNone || hip_runtime_version() >= 70200000 || cap_force);
   for (int k = 0; k < nch; ++k) {
     if (k + 1 < nch) backward(k + 1);
     hipStream_t cs = (two && (k & 1)) ? s_comp2_ : s_comp_;
@@ -1303,6 +1328,11 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     src.self_field_stride = dst.self_field_stride = static_cast<long long>(spec_);
     CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
   }
+  // combine inputs: received blocks in the exchange buffer (five fields), own blocks in place
+  for (int j = 0; j < kBwdFields; ++j) {
+    src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
+    if (self_direct_) src.self_fld[j] = in_field(j);
+  }
   ZArgs za = za0;
   za.NX = p.nx_loc;
   za.field_stride = static_cast<long long>(zstride_);
@@ -1383,7 +1413,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
       ev(4, false, s_comm_);
-      a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+      a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
       ev(4, true, s_comm_);
     }
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
@@ -1392,7 +1422,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
   }
   for (int t = 0; t < nch + 6; ++t) {
-    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_rows(t * ch, ch, true, 6, bchunk, NB); });
+    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_rows(t * ch, ch, true, kBwdFields, bchunk, NB); });
     if (t - 2 >= 0 && t - 2 < nch) comm_op(t - 2, E_XB, E_B, [&] { b2b_pencil_chunk(t - 2, ch, true, 6); });
     if (t - 4 >= 0 && t - 4 < nch) comm_op(t - 4, E_Z, E_BF, [&] { b2b_pencil_chunk(t - 4, ch, false, 3); });
     if (t - 6 >= 0 && t - 6 < nch) comm_op(t - 6, E_XF, -1, [&] { a2a_slab_chunk(t - 6, ch, false, 3); });
@@ -1450,7 +1480,7 @@ void Solver::presend_backward(bool wait_blocks) {
   for (int b = 0; b + 1 < nkb_; ++b) {
     if (wait_blocks) HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
     ev(4, false, s_comm_);
-    a2a_slab_rows(0, maxrows, true, 6, b, b + 1);
+    a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
     ev(4, true, s_comm_);
   }
   HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
@@ -1539,6 +1569,12 @@ void Solver::step(bool stats_for_next) {
           throw;
         }
         HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
+        // CHANNEL_GRAPH_DOT=<prefix>: the captured step graph as <prefix>_r<rank>_g<gi>.dot (topology
+        // diagnosis: which nodes and cross-stream edges a replay has to honour)
+        if (const char* dp = std::getenv("CHANNEL_GRAPH_DOT")) {
+          const std::string path = std::string(dp) + "_r" + std::to_string(plan_.rank) + "_g" + std::to_string(gi) + ".dot";
+          if (hipGraphDebugDotPrint(g, path.c_str(), 0) != hipSuccess) (void)hipGetLastError();
+        }
         HIP_CHECK(hipGraphInstantiate(&gexec_[gi], g, nullptr, nullptr, 0));
         (void)hipGraphDestroy(g);
       } catch (const Error& e) {
@@ -2058,9 +2094,11 @@ Solver::Spectra Solver::spectra() {
   HIP_CHECK(hipMemsetAsync(d_spec_, 0, (nx + nz + nm) * sizeof(double), s_comp_));
   HIP_CHECK(hipMemcpyAsync(planes, out.planes.data(), np * sizeof(int), hipMemcpyHostToDevice, s_comp_));
   SpectraArgs a;
-  a.u = field_ptr(OUT0);
+  a.dv = field_ptr(OUT0);
   a.v = field_ptr(OUT1);
-  a.w = field_ptr(OUT2);
+  a.om = field_ptr(OMEGA);
+  a.ax = p.ax;
+  a.az = p.az;
   a.lines = p.nkx_loc * nkzs_;
   a.nkx_loc = p.nkx_loc;
   a.kx0 = p.kx0;
@@ -2079,9 +2117,9 @@ Solver::Spectra Solver::spectra() {
   for (int b = 0; b < nkb_; ++b) {  // per kx sub-block (accumulating; map rows are disjoint)
     SpectraArgs ab = a;
     const size_t off = kb_off_[b] * esz_;
-    ab.u = static_cast<const char*>(a.u) + off;
+    ab.dv = static_cast<const char*>(a.dv) + off;
     ab.v = static_cast<const char*>(a.v) + off;
-    ab.w = static_cast<const char*>(a.w) + off;
+    ab.om = static_cast<const char*>(a.om) + off;
     ab.lines = kb_cnt_[b] * nkzs_;
     ab.nkx_loc = kb_cnt_[b];
     ab.kx0 = p.kx0 + kb_start_[b];

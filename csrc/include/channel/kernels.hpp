@@ -111,9 +111,10 @@ struct SpecArgs {
   void* omega = nullptr;  // line (0,0) holds U(y)
   void* Rphi = nullptr;
   void* Romega = nullptr;
-  void* out[6] = {};      // u, v, w, omega_x, omega_y, omega_z ; out[0..2] double as H_x,H_y,H_z input
-                          // (out[4] == omega: the state IS the omega_y output, nothing is stored
-                          // there; the x transform zeroes its mean line, see XArgs::zero_mean_field)
+  void* out[6] = {};      // outputs D1 v, v, D1 omega (out[0..2]; they double as the H_x, H_y, H_z
+                          // inputs); out[4] == omega (the state is the omega_y source); out[3] and
+                          // out[5] are unused: the x-backward forms u, w, omega_x, omega_z from
+                          // D1 v, omega, phi, D1 omega (XArgs::combine)
   int store_r = 1;        // 0: skip the R_phi/R_omega stores (last substep: the next one has zeta = 0)
   int lds_poison = 0;     // debug: fill the LDS with NaN before use (CHANNEL_LDS_POISON)
   // diagnostics
@@ -145,6 +146,10 @@ struct Twiddles {
 constexpr int kMaxSeg = 16;
 struct XSrc {
   const void* base = nullptr;
+  // combine mode (XArgs::combine): input field j (0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi) at fld[j]
+  // (the exchange blocks or the spectral field: base is unused) and its self blocks at self_fld[j]
+  const void* fld[5] = {};
+  const void* self_fld[5] = {};
   int nsrc = 1;
   int kx_start[kMaxSeg + 1] = {0};   // global retained-kx start of source s (kx_start[nsrc] = nkx)
   long long off[kMaxSeg] = {0};      // element offset of source block s
@@ -186,13 +191,18 @@ struct XArgs {
   int kzb = 0, nkzs = 0, spec_y0 = 0;
   int nt = 0;                        // streaming (non-temporal) spectral accesses (solver default 1;
                                      // CHANNEL_XNT=0 off: 35.0 vs 34.75 ms/step, profiles/r04/ab_xnt.txt)
+  // backward only: combine mode -- the six output fields u, v, w, omega_x, omega_y, omega_z are
+  // formed per element from the five inputs XSrc::fld (D1 v, v, D1 omega, omega, phi; fft_impl.hpp
+  // cmb_pair); ax, az = 2 pi / LX, 2 pi / LZ (the kx of retained row i, the kz of kz_glob0 + kz)
+  int combine = 0;
+  double ax = 1.0, az = 2.0;
 };
 // backward: spectral (truncated kx) -> [y][x][kz] complex, zero padding kx
 void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, bool fp64, hipStream_t s);
 // forward: [y][x][kz] -> spectral truncated kx (unnormalised)
 void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s);
 // template arguments of this thread's last x-transform launch, in rocprofv3's kernel-name form (tests)
-std::string& xfft_last_variant();
+std::string xfft_last_variant();
 
 struct ZArgs {
   int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;   // NX = local x count (rows = ny * NX)
@@ -243,7 +253,10 @@ void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool
 
 // ---- diagnostics ---------------------------------------------------------------------------
 struct SpectraArgs {
-  const void *u = nullptr, *v = nullptr, *w = nullptr;  // spectral [NY][lines], lines = nkx_loc*nkz_loc
+  // spectral [NY][lines] fields, lines = nkx_loc*nkz_loc: the K-SPEC outputs D1 v, v and the omega
+  // state; u = i (al D1v - be om)/k2 and w = i (be D1v + al om)/k2 are formed per element
+  const void *dv = nullptr, *v = nullptr, *om = nullptr;
+  double ax = 1.0, az = 2.0;
   int lines = 0, nkx_loc = 0, kx0 = 0, nkz_loc = 0, kz0 = 0;
   int nkzs = 0, kzb = 0;              // line stride in kz, layout (spec_index)
   int nkx = 0, Kx = 0, nkz = 0;       // global retained counts

@@ -127,6 +127,9 @@ class Solver {
   // ---- raw device access (tests / bindings) ----------------------------------------------
   enum Field { PHI = 0, OMEGA, RPHI, ROMEGA, OUT0, OUT1, OUT2, OUT3, OUT4, OUT5 };
   void* field_ptr(int f) const;
+  // input j of the x-backward's combine mode (0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi)
+  static constexpr int kBwdFields = 5;
+  void* in_field(int j) const;
   void* phys_ptr() const { return phys_; }
   const YTablesDev& ytables() const { return ytab_; }
   // kx sub-blocks of the local spectral layout (1 = plain [y][kx_local][kz]; see nkb_)

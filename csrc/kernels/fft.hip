@@ -9,9 +9,17 @@ using namespace dev;
 
 static void build_reg_twiddles(int n, bool fp64, void** out);
 
-std::string& xfft_last_variant() {
-  static thread_local std::string v;
+XVariant& xfft_variant_slot() {
+  static thread_local XVariant v;
   return v;
+}
+std::string xfft_last_variant() {
+  const XVariant& v = xfft_variant_slot();
+  std::string s = std::string(v.kernel) + "<" + std::to_string(v.nn) + ", " + (v.f64 ? "double" : "float") + ", " +
+                  (v.seg ? "true" : "false") + ", " + std::to_string(v.wide) + ", " + std::to_string(v.sm) + ", " +
+                  std::to_string(v.v) + ", " + std::to_string(v.sl);
+  if (v.cmb >= 0) s += v.cmb ? ", true" : ", false";
+  return s + ">";
 }
 
 void Twiddles::build(int n_, bool fp64_) {
@@ -98,13 +106,19 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
   // the first pass skips the zero band of the 2/3 rule at compile time (wave_pass ZB)
   CH_CHECK(a.Kx == a.NX / 3 && a.nkx == 2 * a.Kx + 1, "xfft_backward: retained kx must be the 2/3 rule's (Kx = NX/3)");
-  CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
+  CH_CHECK(a.combine || a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
+  if (a.combine) {
+    for (int j = 0; j < kCmbInputs; ++j)
+      CH_CHECK(src.fld[j] && (src.self_seg < 0 || src.self_fld[j]), "xfft_backward: combine mode input field " << j << " missing");
+  }
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz < (1LL << 32), "xfft_backward: per-field plane block exceeds 32-bit offsets");
   // one-source / blocked-layout paths address with 32-bit BYTE offsets (fft_impl.hpp at_byte)
   const long long esz = fp64 ? 16 : 8;
   CH_CHECK(static_cast<long long>(a.ny) * a.NX * a.nkz * esz < (1LL << 32),
            "xfft_backward: a field's x-expanded chunk exceeds 4 GiB (use smaller y chunks)");
-  CH_CHECK(!a.kzb || a.field_stride_spec * esz < (1LL << 32), "xfft_backward: blocked spectral field exceeds 4 GiB");
+  CH_CHECK(!a.kzb || (a.combine ? static_cast<long long>(spec_rows(kSpecKzBlock, a.spec_y0 + a.ny)) * a.nkx * a.nkzs
+                               : a.field_stride_spec) * esz < (1LL << 32),
+           "xfft_backward: blocked spectral field exceeds 4 GiB");
   CH_CHECK(src.nsrc > 1 || src.self_seg >= 0 || static_cast<long long>(a.ny) * a.nkx * a.nkz * esz < (1LL << 32),
            "xfft_backward: a field's spectral chunk exceeds 4 GiB (use smaller y chunks)");
   CH_DISPATCH_N(a.NX, fft_xb_len<NN>(a, src, phys, tw, fp64, s));

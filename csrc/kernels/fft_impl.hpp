@@ -244,6 +244,41 @@ __device__ __forceinline__ void st_nt(P& r, const P& v) {
   }
 }
 
+// Combine mode of the x-backward (XArgs::combine): K-SPEC writes v, D1 v, D1 omega next to the
+// states omega and phi, and the gather forms the six fields of the physical-space stage in
+// registers, per element (kspec_kernel; nonLinear_kernels.cu:55-72, convolution_kernels.cu:46-53):
+//   u  = i (al D1v - be om)/k2        w  = i (be D1v + al om)/k2
+//   wx = i (be phi + al D1om)/k2      wz = i (be D1om - al phi)/k2   (D2 v = phi + k2 v)
+//   v = v, wy = om; on the mean line (kx = kz = 0) u = U = Re om, wz = -dU/dy, wy = 0.
+// A tile of group g holds two output fields (kCmbOutA/B[g], CL columns each) formed from two input
+// fields (kCmbInP/Q[g]) loaded at the same elements.  Input fields: 0 D1 v, 1 v, 2 D1 omega,
+// 3 omega, 4 phi (XSrc::fld).
+// Groups 0 (u, w from D1 v, omega) and 1 (v, omega_y from v, omega) are adjacent in the tile order,
+// so the second read of omega's chunk follows the first (from the Infinity Cache).
+constexpr int kCmbGroups = 3, kCmbInputs = 5;
+__host__ __device__ constexpr int cmb_in_p(int g) { return g == 0 ? 0 : (g == 1 ? 1 : 4); }
+__host__ __device__ constexpr int cmb_in_q(int g) { return g == 2 ? 2 : 3; }
+__host__ __device__ constexpr int cmb_out_a(int g) { return g == 0 ? 0 : (g == 1 ? 1 : 3); }
+__host__ __device__ constexpr int cmb_out_b(int g) { return g == 0 ? 2 : (g == 1 ? 4 : 5); }
+template <typename T>
+__device__ __forceinline__ T cmb_rcp(T k2) {
+  if constexpr (sizeof(T) == 4) return k2 > 0.f ? __builtin_amdgcn_rcpf(k2) : 0.f;
+  else return k2 > 0.0 ? 1.0 / k2 : 0.0;
+}
+template <typename T2, typename T>
+__device__ __forceinline__ void cmb_pair(int g, T2 P, T2 Q, T al, T be, T r, bool mean, T2& A, T2& B) {
+  if (g == 0) {  // u, w from (D1 v, omega)
+    A = T2{-(al * P.y - be * Q.y) * r + (mean ? Q.x : T(0)), (al * P.x - be * Q.x) * r};
+    B = T2{-(be * P.y + al * Q.y) * r, (be * P.x + al * Q.x) * r};
+  } else if (g == 2) {  // omega_x, omega_z from (phi, D1 omega)
+    A = T2{-(be * P.y + al * Q.y) * r, (be * P.x + al * Q.x) * r};
+    B = T2{-(be * Q.y - al * P.y) * r - (mean ? Q.x : T(0)), (be * Q.x - al * P.x) * r};
+  } else {  // v, omega_y from (v, omega)
+    A = P;
+    B = mean ? T2{0, 0} : Q;
+  }
+}
+
 // Both x kernels are persistent: the grid is the resident capacity (2 blocks per CU, bounded by
 // LDS) and each block walks (field, y, kz-chunk) tiles.  The next tile's global loads are issued
 // into registers right after the current tile is staged into LDS, so they are in flight during
@@ -256,19 +291,25 @@ __device__ __forceinline__ void st_nt(P& r, const P& v) {
 // same layout with the C columns of a tile taken as C / 8 planes x one 8-wide kz block: each
 // retained kx then contributes one contiguous piece of C / 8 rows of the block (128 bytes, a whole
 // line, for the 16-column tiles) instead of 64-byte halves read by two tiles.
-template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
+// CMB: combine mode (above): a tile is one group, CL = C / 2 columns of each of its two outputs,
+// each thread loading its elements of both inputs (SL = 2: one plane x one 8-wide kz block; the
+// neighbouring plane's tile, the next one in the XCD's order, reads the other half of the lines).
+template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0, bool CMB = false>
 __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::MINB))
     xfft_backward_kernel(XArgs a, XSrc src, typename C2<T>::type* phys, const typename C2<T>::type* tw) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NX, T, WIDE>;
   using CV = CVec<T2, V>;
-  using QM = XQuad<NX, T, WIDE, SL, V>;
+  using QM = XQuad<NX, T, WIDE, CMB ? 0 : SL, V>;
   constexpr int C = Cfg::C, NT = Cfg::NT, PITCH = QM::PITCH;
-  constexpr int CW = C / V;  // accesses per tile row (V kz columns each; the host checks nkz % V == 0)
-  // only the retained kx are loaded (nkx*C elements); the zero padding is re-written in LDS
+  constexpr int CL = CMB ? C / 2 : C;  // loaded columns per input field
+  static_assert(!CMB || (C % (2 * V) == 0), "combine mode: two halves of whole accesses");
+  constexpr int CW = CL / V;  // accesses per tile row and input (V kz columns each; the host checks nkz % V == 0)
+  // only the retained kx are loaded (nkx*CL elements per input); the zero padding is re-written in LDS
   constexpr int NKMAX = 2 * (NX / 3) + 1;
   constexpr int NKX = NKMAX, KXH = NX / 3;  // retained kx: the 2/3 rule's (checked on the host)
   constexpr int EPT = (NKMAX * CW + NT - 1) / NT;
+  constexpr int NIN = CMB ? 2 : 1;  // input fields per tile
   __shared__ T2 s[C * PITCH];
   constexpr int TS = FftPlan<NX>::TSIZE;
   __shared__ T2 tws[TS];
@@ -278,27 +319,29 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     __syncthreads();
   }
   for (int i = threadIdx.x; i < TS; i += NT) tws[i] = tw[i];
-  // tile = YP planes x KC kz columns (column c: plane y0 + c / KC, kz kz0 + c % KC)
-  constexpr int KC = SL == 2 ? kSpecKzBlock : C, YP = C / KC;
-  static_assert(SL != 2 || C % kSpecKzBlock == 0, "plane tiles need whole kz blocks");
+  // tile = YP planes x KC kz columns (column c: plane y0 + c / KC, kz kz0 + c % KC; CMB: c % CL)
+  constexpr int KC = SL == 2 ? kSpecKzBlock : CL, YP = CL / KC;
+  static_assert(SL != 2 || CL % kSpecKzBlock == 0, "plane tiles need whole kz blocks");
   const int nkzc = (a.nkz + KC - 1) / KC, nyt = (a.ny + YP - 1) / YP;
-  const int ntiles = nyt * nkzc * a.nfields;
+  const int nf = CMB ? kCmbGroups : a.nfields;
+  const int ntiles = nyt * nkzc * nf;
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
   const int nload = NKX * CW;
-  CV v[EPT];
+  CV v[NIN][EPT];
   static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
   static_assert(SM != kSegRows || (NT % CW == 0 && EPT <= kSegRowsMax), "row table: a thread's rows repeat per access");
   SegRows<SM == kSegRows ? EPT : 1> rt;
   if constexpr (SM == kSegRows)
     rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, a.nkz, tid);
   // SEG (pencil: the x-expanded output blocked by x range) with row tables: the thread's x rows
-  // x = (tid + k NT) / CW of the store passes, looked up once like the kx rows
-  constexpr int KXS = (NX * CW + NT - 1) / NT;
+  // x = (tid + k NT) / CWO of the store passes, looked up once like the kx rows
+  constexpr int CWO = C / V;  // store accesses per x row (both halves in CMB mode)
+  constexpr int KXS = (NX * CWO + NT - 1) / NT;
   constexpr bool kXRows = SEG && SM == kSegRows;
   static_assert(!kXRows || KXS <= kSegRowsMax, "x row table too long");
   SegRows<kXRows ? KXS : 1> xt;
-  if constexpr (kXRows) xt.template build<NT, CW, NX, 8>(a.x_start, a.poff, a.npseg, -1, 0, a.nkz, tid);
+  if constexpr (kXRows) xt.template build<NT, CWO, NX, 8>(a.x_start, a.poff, a.npseg, -1, 0, a.nkz, tid);
   // tile t -> (f, y0, kz0); at each iteration the blocks of one XCD take consecutive tiles
   auto decode = [&](int t, int& f, int& y, int& kz0) {
     if constexpr (SL) {
@@ -307,68 +350,80 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       kz0 = (rest % nkzc) * KC;
       f = rest / nkzc;
     } else {
-      kz0 = (t % nkzc) * C;
+      kz0 = (t % nkzc) * CL;
       const int rest = t / nkzc;
       y = rest % a.ny;
       f = rest / a.ny;
     }
   };
+  // spectral base of input k (0: P, 1: Q) of tile field / group f, and of its self blocks
+  auto in_base = [&](int f, int k) -> const T2* {
+    if constexpr (CMB) return static_cast<const T2*>(src.fld[k ? cmb_in_q(f) : cmb_in_p(f)]);
+    else return static_cast<const T2*>(src.base) + f * a.field_stride_spec;
+  };
+  auto in_self = [&](int f, int k) -> const T2* {
+    if constexpr (CMB) return static_cast<const T2*>(src.self_fld[k ? cmb_in_q(f) : cmb_in_p(f)]);
+    else return static_cast<const T2*>(src.self_base) + f * src.self_field_stride;
+  };
   auto fetch = [&](int t) {
     int f, y, kz0;
     decode(t, f, y, kz0);
-    const T2* base = static_cast<const T2*>(src.base) + f * a.field_stride_spec;
-    if constexpr (SL) {
-      // each thread keeps one column (plane, kz) and walks kx rows i0 + q NT/CW, one block column
-      // stride apart; the retained kx count is NKMAX (checked on the host), so only the rows of the
-      // last accesses can pass it
-      static_assert(NT % CW == 0, "a thread's column must be the same for every access");
-      constexpr int DI = NT / CW;
-      const int c = (QM::on ? quad_col(tid) : tid % CW) * V, r0 = QM::on ? quad_row(tid) : tid / CW;
-      const unsigned bt = spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V)) *
-                          static_cast<unsigned>(sizeof(T2));
-      const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
-      const CV* bv = reinterpret_cast<const CV*>(base);
-      if (a.nt) {
 #pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-          int i = r0 + q * DI;
-          if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
-          v[q] = ld_nt(at_byte(bv, bt + static_cast<unsigned>(i) * rs));
-        }
-      } else {
+    for (int k = 0; k < NIN; ++k) {
+      const T2* base = in_base(f, k);
+      if constexpr (SL) {
+        // each thread keeps one column (plane, kz) and walks kx rows i0 + q NT/CW, one block column
+        // stride apart; the retained kx count is NKMAX (checked on the host), so only the rows of
+        // the last accesses can pass it
+        static_assert(NT % CW == 0, "a thread's column must be the same for every access");
+        constexpr int DI = NT / CW;
+        const int c = (QM::on ? quad_col(tid) : tid % CW) * V, r0 = QM::on ? quad_row(tid) : tid / CW;
+        const unsigned bt = spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V)) *
+                            static_cast<unsigned>(sizeof(T2));
+        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
+        const CV* bv = reinterpret_cast<const CV*>(base);
+        if (a.nt) {
 #pragma unroll
-        for (int q = 0; q < EPT; ++q) {
-          int i = r0 + q * DI;
-          if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
-          v[q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
+          for (int q = 0; q < EPT; ++q) {
+            int i = r0 + q * DI;
+            if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
+            v[k][q] = ld_nt(at_byte(bv, bt + static_cast<unsigned>(i) * rs));
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) {
+            int i = r0 + q * DI;
+            if ((q + 1) * DI > NKMAX) i = min(i, NKMAX - 1);
+            v[k][q] = at_byte(bv, bt + static_cast<unsigned>(i) * rs);
+          }
         }
+        continue;
       }
-      return;
-    }
-    // this rank's own block is read in place from its spectral field (no self exchange)
-    const T2* sbase = src.self_seg >= 0 ? static_cast<const T2*>(src.self_base) + f * src.self_field_stride : base;
+      // this rank's own block is read in place from its spectral field (no self exchange)
+      const T2* sbase = src.self_seg >= 0 ? in_self(f, k) : base;
 #pragma unroll
-    for (int q = 0; q < EPT; ++q) {
-      const int e = tid + q * NT;
-      // unconditional load from a clamped valid address: rows i >= nkx are never staged,
-      // columns kz >= nkz are transformed (independently) but never stored
-      const int i = min(e / CW, NKX - 1);
-      const int c = (e % CW) * V;
-      const int kz = min(kz0 + c % KC, a.nkz - V);
-      if constexpr (SM == kSegOne) {
-        const CV& r = at_byte(reinterpret_cast<const CV*>(base),
-                              (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
-                                  static_cast<unsigned>(sizeof(T2)));
-        v[q] = a.nt ? ld_nt(r) : r;
-      } else if constexpr (SM == kSegRows) {
-        v[q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, y, kz));
-      } else {
-        const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
-                                        : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
-        const T2* b = static_cast<unsigned>(sp.idx - src.self_seg) < static_cast<unsigned>(src.nself) ? sbase : base;
-        // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
-        v[q] = *reinterpret_cast<const CV*>(
-            b + static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz));
+      for (int q = 0; q < EPT; ++q) {
+        const int e = tid + q * NT;
+        // unconditional load from a clamped valid address: rows i >= nkx are never staged,
+        // columns kz >= nkz are transformed (independently) but never stored
+        const int i = min(e / CW, NKX - 1);
+        const int c = (e % CW) * V;
+        const int kz = min(kz0 + c % KC, a.nkz - V);
+        if constexpr (SM == kSegOne) {
+          const CV& r = at_byte(reinterpret_cast<const CV*>(base),
+                                (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) + static_cast<unsigned>(kz)) *
+                                    static_cast<unsigned>(sizeof(T2)));
+          v[k][q] = a.nt ? ld_nt(r) : r;
+        } else if constexpr (SM == kSegRows) {
+          v[k][q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, y, kz));
+        } else {
+          const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
+                                          : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
+          const T2* b = static_cast<unsigned>(sp.idx - src.self_seg) < static_cast<unsigned>(src.nself) ? sbase : base;
+          // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
+          v[k][q] = *reinterpret_cast<const CV*>(
+              b + static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz));
+        }
       }
     }
   };
@@ -380,17 +435,34 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     lds_barrier();  // previous tile's stores have finished reading s
     // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
     // state, whose mean line holds U(y)); it is kx row i = 0, the kz-0 column of each plane
-    const bool zmean = f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
+    const bool zmean = !CMB && f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      const int i = QM::on ? quad_row(tid) + q * (NT / CW) : e / CW;
-      const int c = (QM::on ? quad_col(tid) : e - (e / CW) * CW) * V;
+      const int i = QM::on ? quad_row(tid) + q * (NT / CW) : (SL ? tid / CW + q * (NT / CW) : e / CW);
+      const int c = (QM::on ? quad_col(tid) : (SL ? tid % CW : e - (e / CW) * CW)) * V;
       const int x = i <= KXH ? i : NX - (NKX - i);
-      if (QM::on ? i < NKX : e < nload)
+      if (QM::on || SL ? i < NKX : e < nload) {
+        if constexpr (CMB) {
+          // the two outputs of the group from the two inputs (wavenumbers of this element)
+          const int kxs = i <= KXH ? i : i - NKX;
+          const T al = static_cast<T>(a.ax * kxs);
 #pragma unroll
-        for (int u = 0; u < V; ++u)
-          s[(c + u) * PITCH + fft_pidx(x)] = (zmean && i == 0 && (c + u) % KC == 0) ? T2{0, 0} : v[q].c[u];
+          for (int u = 0; u < V; ++u) {
+            const int kzg = a.kz_glob0 + kz0 + (c + u) % KC;
+            const T be = static_cast<T>(a.az * kzg);
+            const T r = cmb_rcp<T>(al * al + be * be);
+            T2 A, B;
+            cmb_pair<T2, T>(f, v[0][q].c[u], v[1][q].c[u], al, be, r, i == 0 && kzg == 0, A, B);
+            s[(c + u) * PITCH + fft_pidx(x)] = A;
+            s[(CL + c + u) * PITCH + fft_pidx(x)] = B;
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < V; ++u)
+            s[(c + u) * PITCH + fft_pidx(x)] = (zmean && i == 0 && (c + u) % KC == 0) ? T2{0, 0} : v[0][q].c[u];
+        }
+      }
     }
     // zero padding: only the band elements the first pass reads (its input blocks that straddle
     // the band edges; the blocks inside the band are compile-time zeros, wave_pass ZB)
@@ -420,29 +492,35 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           wave_fft<NX, RB, PITCH, true, TPR, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
-    T2* out = phys + f * a.field_stride_phys;
+    // output field of LDS column c (CMB: the group's two outputs) and its kz / plane
+    const int fa = CMB ? cmb_out_a(f) : f, fb = CMB ? cmb_out_b(f) : f;
+    T2* outa = phys + fa * a.field_stride_phys;
+    T2* outb = phys + fb * a.field_stride_phys;
     if constexpr (kXRows) {
 #pragma unroll
       for (int k = 0; k < KXS; ++k) {
         const int e = tid + k * NT;
-        const int x = e / CW, c = (e - x * CW) * V;
-        const int kz = kz0 + c % KC, yy = y + c / KC;
-        if (e < NX * CW && kz < a.nkz && yy < a.ny) {
+        const int x = e / CWO, c = (e - x * CWO) * V;
+        const int cc = c % CL;
+        const int kz = kz0 + cc % KC, yy = y + cc / KC;
+        if (e < NX * CWO && kz < a.nkz && yy < a.ny) {
           CV w;
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          *reinterpret_cast<CV*>(out + xt.at(k, yy, kz)) = w;
+          *reinterpret_cast<CV*>((c < CL ? outa : outb) + xt.at(k, yy, kz)) = w;
         }
       }
       continue;
     }
-    for (int e = tid; e < NX * CW; e += NT) {
-      const int x = e / CW, c = (e - x * CW) * V;
-      const int kz = kz0 + c % KC, yy = y + c / KC;
+    for (int e = tid; e < NX * CWO; e += NT) {
+      const int x = e / CWO, c = (e - x * CWO) * V;
+      const int cc = c % CL;
+      const int kz = kz0 + cc % KC, yy = y + cc / KC;
       if (kz < a.nkz && yy < a.ny) {
         CV w;
 #pragma unroll
         for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+        T2* out = c < CL ? outa : outb;
         if constexpr (SEG) {
           const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
           *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
@@ -626,13 +704,18 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 }
 
 // The template arguments of the last x-transform launch of this thread, as in the rocprofv3 kernel
-// names ("xfft_backward_kernel<1024, float, false, 1, 0, 2, 2>"): tests assert that they exercise
-// the variant the headline grid runs (profiles/r04/final2/kernel_stats_1024x385x1024.csv)
-std::string& xfft_last_variant();
-inline void xfft_note_variant(const char* k, int nn, bool f64, bool seg, int wide, int sm, int v, int sl) {
-  xfft_last_variant() = std::string(k) + "<" + std::to_string(nn) + ", " + (f64 ? "double" : "float") + ", " +
-                        (seg ? "true" : "false") + ", " + std::to_string(wide) + ", " + std::to_string(sm) + ", " +
-                        std::to_string(v) + ", " + std::to_string(sl) + ">";
+// names ("xfft_backward_kernel<1024, float, false, 1, 0, 2, 2, true>"): tests assert that they
+// exercise the variant the headline grid runs.  Recorded as plain values on the launch path and
+// formatted only when asked for (xfft_last_variant).
+struct XVariant {
+  const char* kernel = "";
+  int nn = 0, wide = 0, sm = 0, v = 0, sl = 0;
+  bool f64 = false, seg = false;
+  int cmb = -1;  // -1: the kernel has no combine argument (the forward)
+};
+XVariant& xfft_variant_slot();
+inline void xfft_note_variant(const char* k, int nn, bool f64, bool seg, int wide, int sm, int v, int sl, int cmb = -1) {
+  xfft_variant_slot() = XVariant{k, nn, wide, sm, v, sl, f64, seg, cmb};
 }
 
 // Persistent grid of a transform kernel: the resident capacity, or fewer blocks per CU when
@@ -668,32 +751,57 @@ template <int NN, typename T, int WIDE, int V = 1>
 static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw, hipStream_t s) {
   using T2 = typename C2<T>::type;
   using Cfg = XCfg<NN, T, WIDE>;
-  if constexpr (V == 1 && sizeof(T) == 4 && Cfg::C % 2 == 0) {
-    if (xvec_ok(a, src.off, src.nsrc, src.self_field_stride, 0)) return xb_launch_cfg<NN, T, WIDE, 2>(a, src, phys, tw, s);
+  if constexpr (V == 1 && sizeof(T) == 4 && Cfg::C % 4 == 0) {
+    bool ok = xvec_ok(a, src.off, src.nsrc, src.self_field_stride, 0);
+    if (a.combine)  // (every input field pointer 16-byte aligned)
+      for (int j = 0; j < kCmbInputs; ++j)
+        ok = ok && reinterpret_cast<uintptr_t>(src.fld[j]) % 16 == 0 &&
+             (src.self_seg < 0 || reinterpret_cast<uintptr_t>(src.self_fld[j]) % 16 == 0);
+    if (ok) return xb_launch_cfg<NN, T, WIDE, 2>(a, src, phys, tw, s);
   }
+  // combine mode: two halves of C / 2 columns (the loaded columns per input field)
+  constexpr int CL = Cfg::C / 2;
+  constexpr int CWC = CL / V;
   // (no window variant here: the fetch is unrolled over the tile, and the scalar lookups of all
   // its windows, computed up front, spilled ~640 SGPRs)
-  const int sm = seg_mode<Cfg::NT, Cfg::C / V>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
+  const int sm = seg_mode<Cfg::NT, CWC>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
   CH_CHECK(!a.kzb || (sm == kSegOne && a.npseg == 1 && a.nkzs % kSpecKzBlock == 0),
            "xfft_backward: the blocked spectral layout needs one source block");
-  constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;  // blocked layout: plane tiles when wide
+  // blocked layout: plane tiles when wide (combine: one plane of one 8-wide kz block per half)
+  constexpr int SLB = (WIDE && Cfg::C % kSpecKzBlock == 0) ? 2 : 1;
+  constexpr int SLC = (WIDE && CL % kSpecKzBlock == 0) ? 2 : 1;
   // (row tables where a thread has at most kSegRowsMax rows: 2 VGPRs per row)
-  constexpr int kRowsK = ((2 * (NN / 3) + 1) * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
-  constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % (Cfg::C / V) == 0) ? kSegRows : kSegFull;
+  constexpr int kRowsK = ((2 * (NN / 3) + 1) * CWC + Cfg::NT - 1) / Cfg::NT;
+  constexpr int SMR = (kRowsK <= kSegRowsMax && Cfg::NT % CWC == 0) ? kSegRows : kSegFull;
   const bool rows = SMR == kSegRows && xsegrows_enabled();
   constexpr int kXRowsK = (NN * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
   constexpr int SMX = (SMR == kSegRows && kXRowsK <= kSegRowsMax) ? kSegRows : kSegFull;
-  auto kern = a.kzb           ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
-              : a.npseg > 1   ? (rows ? xfft_backward_kernel<NN, T, true, WIDE, SMX, V>
-                                      : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V>)
-              : sm == kSegOne ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V>
-              : rows          ? xfft_backward_kernel<NN, T, false, WIDE, SMR, V>
-                              : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V>;
-  const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
-  const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
-  xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb || a.npseg > 1 ? (a.kzb ? kSegOne : (rows ? SMX : kSegFull)) : (sm == kSegOne ? kSegOne : (rows ? kSegRows : kSegFull)), V,
-                    a.kzb ? SLB : 0);
+  decltype(&xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 0, true>) kern;
+  int smv = kSegOne, slv = 0;
+  if (a.combine) {
+    CH_CHECK(a.nfields == 6, "xfft_backward: the combine mode forms the six physical-stage fields");
+    if (a.kzb) {
+      kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLC, true>;
+      slv = SLC;
+    } else if (a.npseg > 1) {
+      kern = rows ? xfft_backward_kernel<NN, T, true, WIDE, SMX, V, 0, true> : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V, 0, true>;
+      smv = rows ? SMX : kSegFull;
+    } else if (sm == kSegOne) {
+      kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 0, true>;
+    } else {
+      kern = rows ? xfft_backward_kernel<NN, T, false, WIDE, SMR, V, 0, true> : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V, 0, true>;
+      smv = rows ? kSegRows : kSegFull;
+    }
+  } else {
+    // one field per column (tests, and the single-block paths)
+    CH_CHECK(sm == kSegOne && a.npseg == 1 && src.self_seg < 0, "xfft_backward: exchange segments need the combine mode");
+    kern = a.kzb ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB, false> : xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 0, false>;
+    slv = a.kzb ? SLB : 0;
+  }
+  const int cl = a.combine ? CL : Cfg::C;
+  const int kc = slv == 2 ? kSpecKzBlock : cl, yp = cl / kc;
+  const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * (a.combine ? kCmbGroups : a.nfields);
+  xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, !a.kzb && a.npseg > 1, WIDE, smv, V, slv, a.combine ? 1 : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
 }
@@ -959,7 +1067,7 @@ __global__ void __launch_bounds__(ZWT * TPRT) __attribute__((amdgpu_waves_per_eu
   constexpr bool kPrefetch = sizeof(T) == 4 && NZP <= 1024 && !SEG;
   T2 pa[kPrefetch ? MK : 1], pb[kPrefetch ? MK : 1];
   // the middle pass's twiddles in registers (fp32 register-edge rows: 30 VGPRs against 15 LDS reads
-  // per transform; CHANNEL_ZMIDTW=0 keeps the LDS reads, A/B)
+  // per transform; only in the CHANNEL_ZFFT=1 plan -- ZFFT=0 keeps the LDS reads, A/B)
   constexpr bool kMidReg = kRegEdge && MidTw<NZP>::ok && sizeof(T) == 4 && ZF == 1;
   T2 twm[kMidReg || kR4 ? 15 : 1];
   if constexpr (kMidReg) middle_twiddles<NZP>(tws, twm, lane);

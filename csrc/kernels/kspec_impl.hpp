@@ -9,9 +9,12 @@
 //   calcUW (nonLinear_kernels.cu:8-92), the wz/wx D1 calls and calcOmega
 //   (convolution.c:7-20, convolution_kernels.cu:7-66), calcSt plane sums (statistics.cu:7-95).
 // The reference runs these as ~50 launches + 44 cusparse calls + 8 D2D copies per substep with
-// float<->double casts through HBM.  Here one launch reads 7 fields and writes 10, all y-work is
-// fp64 in registers, and the wall-normal operators are applied in "M-form" (the compact D2 mass
-// matrix multiplies the equation), so the explicit viscous term needs no solve at all.
+// float<->double casts through HBM.  Here one launch reads 7 fields (5 on the first substep) and
+// writes 7 (5 on the last: R_phi, R_omega are not needed there): the states phi and omega, R_phi,
+// R_omega, and v, D1 v, D1 omega, from which the x-backward forms the six fields of the
+// physical-space stage (XArgs::combine).  All y-work is fp64 in registers, and the wall-normal
+// operators are applied in "M-form" (the compact D2 mass matrix multiplies the equation), so the
+// explicit viscous term needs no solve at all.
 //
 // Layout: one wave per line (lane l holds rows l*R .. l*R+R-1), W lines per workgroup, one
 // persistent workgroup per CU walking tiles of W lines.  Per CU the LDS holds the coefficient
@@ -877,7 +880,8 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
           vo[3][r] = om[1][r];
         }
       }
-      st.store(phi, ph);
+      // (STORE2: phi goes out at the end, paired with D1 omega)
+      if constexpr (!kStore2) st.store(phi, ph);
       KSPEC_STAMP(6)
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
@@ -946,7 +950,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     }
     KSPEC_STAMP(7)
     // velocities u = i (al dv - be om)/k2, w = i (be dv + al om)/k2 (nonLinear_kernels.cu:55-72),
-    // formed one output at a time (each is stored before the next is built)
+    // for the plane statistics (the x-backward forms them for the physical-space stage)
     auto vel_u = [&](int r, double& re, double& im) {
       const double ar = (al * dvo[0][r] - be * vo[2][r]) * inv_k2, ai = (al * dvo[1][r] - be * vo[3][r]) * inv_k2;
       re = mf * vo[2][r] - ai;  // mean line: U(y)
@@ -959,7 +963,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     };
     // plane statistics (statistics.cu:7-95), fluctuations only, weight 2 for kz > 0
     if (a.stats) {
-      __syncthreads();  // every wave is done with the tiles (last staging: the phi store)
+      __syncthreads();  // every wave is done with the tiles (last use: the phi store or the omega column)
       for (int i = threadIdx.x; i < 4 * ROWS; i += NT) sred[i] = 0.0;
       __syncthreads();
       if (valid && !is_mean) {
@@ -985,70 +989,28 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
       __syncthreads();  // sred is a staging tile again
     }
     KSPEC_STAMP(8)
-    auto ostore = [&](void* dst, const double (&re)[R], const double (&im)[R], double sc = 1.0) {
-      st.store(static_cast<T2*>(dst), re, im, sc);
-    };
+    // Outputs for the physical-space stage: v, D1 v and D1 omega (+ the omega and phi states).  The
+    // x-backward forms u, w, omega_x, omega_z from them per element (XArgs::combine): u, w from
+    // (D1 v, omega) as above, and with D2 v = phi + k2 v (the Helmholtz identity of the compact D2
+    // operator) omega_x = Dw - i be v = i (be phi + al D1 omega)/k2 and omega_z = i al v - Du =
+    // i (be D1 omega - al phi)/k2 (convolution_kernels.cu:46-53; mean line: u = U, omega_z = -dU/dy).
+    // Three field stores instead of five per substep, and the exchange of P > 1 moves five fields.
     if constexpr (kStore2) {
-      if (a.out[4] == a.omega) {
-        // v and u, then w and omega_x, behind one barrier each (tiles: the extra pair, then the
-        // staging pair, whose last readers (the phi store) passed the first pair's barrier), then
-        // omega_z through the extra tile of the first pair (its readers passed the second barrier)
-        double x[2][R], x2[2][R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
-        st.store2_into(xt0, xt1, static_cast<T2*>(a.out[1]), vo[0], vo[1], static_cast<T2*>(a.out[0]), x[0], x[1]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          vel_w(r, x[0][r], x[1][r]);
-          const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
-          const double br = (be * DDr + al * dvo[2][r]) * inv_k2, bi = (be * DDi + al * dvo[3][r]) * inv_k2;
-          x2[0][r] = -bi + be * vo[1][r];
-          x2[1][r] = br - be * vo[0][r];
-        }
-        st.store2_into(st.tile, st.tile2, static_cast<T2*>(a.out[2]), x[0], x[1], static_cast<T2*>(a.out[3]), x2[0], x2[1]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
-          const double ar = (al * DDr - be * dvo[2][r]) * inv_k2, ai = (al * DDi - be * dvo[3][r]) * inv_k2;
-          x[0][r] = -al * vo[1][r] + ai - mf * dvo[2][r];
-          x[1][r] = al * vo[0][r] - ar;
-        }
-        st.store_into(xt0, static_cast<T2*>(a.out[5]), x[0], x[1]);
+      if (a.mode == 1) {
+        // phi and D1 omega, then v and D1 v, behind one barrier each (tiles: the extra pair, whose
+        // last readers (the R stores) passed the omega store's barrier; then the staging pair, whose
+        // last readers (the omega column) passed the first pair's barrier); the closing barrier
+        // keeps the next tile's first staging behind the second pair's copy-out
+        st.store2_into(xt0, xt1, phi, ph[0], ph[1], static_cast<T2*>(a.out[2]), dvo[2], dvo[3]);
+        st.store2_into(st.tile, st.tile2, static_cast<T2*>(a.out[1]), vo[0], vo[1], static_cast<T2*>(a.out[0]), dvo[0],
+                       dvo[1]);
+        lds_barrier();
         goto outputs_done;
       }
     }
-    ostore(a.out[1], vo[0], vo[1]);  // v
-    // omega_y: when out[4] is the omega state itself (the solver's layout) it is already stored;
-    // the x transform reads its mean line (U) as 0
-    if (a.out[4] != a.omega) ostore(a.out[4], vo[2], vo[3], 1.0 - mf);
-    {
-      double x[2][R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
-      ostore(a.out[0], x[0], x[1]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
-      ostore(a.out[2], x[0], x[1]);
-      // vorticity: wx = Dw - i be v ; wz = i al v - Du   (convolution_kernels.cu:46-53)
-      // D(dv) = D2 v = phi + k2 v (Helmholtz identity, consistent with the compact D2 operator)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
-        const double br = (be * DDr + al * dvo[2][r]) * inv_k2, bi = (be * DDi + al * dvo[3][r]) * inv_k2;
-        x[0][r] = -bi + be * vo[1][r];
-        x[1][r] = br - be * vo[0][r];
-      }
-      ostore(a.out[3], x[0], x[1]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
-        const double ar = (al * DDr - be * dvo[2][r]) * inv_k2, ai = (al * DDi - be * dvo[3][r]) * inv_k2;
-        // Du = i(ar + i ai) = -ai + i ar ; wz = i al v - Du ; mean line: -dU/dy
-        x[0][r] = -al * vo[1][r] + ai - mf * dvo[2][r];
-        x[1][r] = al * vo[0][r] - ar;
-      }
-      ostore(a.out[5], x[0], x[1]);
-    }
+    st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);    // v
+    st.store(static_cast<T2*>(a.out[0]), dvo[0], dvo[1]);  // D1 v
+    st.store(static_cast<T2*>(a.out[2]), dvo[2], dvo[3]);  // D1 omega (mean line: dU/dy)
   outputs_done:
     if (a.mean_diag && is_mean) {
       const double d0 = line_row_value<R, XM>(dvo[2], 0, g, lane), dN = line_row_value<R, XM>(dvo[2], N - 1, g, lane);
@@ -1072,17 +1034,17 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
 #undef KSPEC_STAMP
 }
 
-// K-SPEC output stage (split mode, after kspec_kernel<..., SPLIT = 1>): per line, v (out[1]),
-// omega and phi in, D1 of v and omega (one 4-RHS solve on the constant factorisation), the plane
-// statistics and the u, w, omega_x, omega_z outputs (nonLinear_kernels.cu:8-92,
-// convolution_kernels.cu:7-66, statistics.cu:7-95).  Without the advance's registers (the
+// K-SPEC output stage (split mode, after kspec_kernel<..., SPLIT = 1>): per line, v (out[1]) and
+// omega in, D1 of omega and of v (two 2-RHS solves on the constant factorisation), the plane
+// statistics (statistics.cu:7-95) and the D1 v / D1 omega outputs the x-backward forms u, w,
+// omega_x, omega_z from (nonLinear_kernels.cu:8-92, convolution_kernels.cu:7-66).  Without the advance's registers (the
 // k-dependent factorisations, the 6-RHS implicit solve) a line fits in <= 256 VGPRs at R <= 8, so
 // W = 8 lines per workgroup run two waves per SIMD: the output half of the substep was the
-// latency-bound half at one wave per SIMD (it reads 3 fields more than the fused kernel).
+// latency-bound half at one wave per SIMD (it reads 2 fields more than the fused kernel).
 template <int R, typename T, int W, int XM>
 __global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) {
   using T2 = typename Cplx<T>::type;
-  constexpr int NS = 3;  // one register slot per input: v, omega, phi
+  constexpr int NS = 3;  // register slots 0 (omega) and 2 (v)
   using St = Stage<R, T, W, NS, false>;
   constexpr int ROWS = 64 * R;
   constexpr bool TLDS = kspec_tables_in_lds<R, T, W>();
@@ -1138,13 +1100,11 @@ __global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) 
   st.set_layout(a.kzb);
   const T2* vin = static_cast<const T2*>(a.out[1]);
   const T2* omega = static_cast<const T2*>(a.omega);
-  const T2* phi = static_cast<const T2*>(a.phi);
-  // inputs: omega (slot 0), phi (slot 1), v (slot 2); each slot is refilled with the next tile's
-  // field right after its commit
+  // inputs: omega (slot 0), v (slot 2); each slot is refilled with the next tile's field right
+  // after its commit
   if (lb < ntiles) {
     st.template prefetch_at<0>(omega, lb * W);
     st.template prefetch_at<2>(vin, lb * W);
-    st.template prefetch_at<1>(phi, lb * W);
   }
   for (int tile = lb; tile < ntiles; tile += gridDim.x) {
     const int line0 = tile * W;
@@ -1162,45 +1122,22 @@ __global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) 
     const bool is_mean = valid && kx == 0 && kz == 0;
     const double inv_k2 = k2 > 0.0 ? 1.0 / k2 : 0.0;
     const double mf = is_mean ? 1.0 : 0.0;
-    const double nz = (is_mean || k2 == 0.0) ? 0.0 : 1.0;
 
-    // vorticity first (it needs phi, D1 omega and v), then the velocities (D1 v and omega): two
-    // 2-RHS solves instead of one 4-RHS solve keep phi and D1 omega out of the velocity phase
-    double om[2][R], v[2][R], d[2][R], x[2][R];
+    // D1 omega (mean line: dU/dy), then D1 v: the outputs of the physical-space stage besides v and
+    // the states (the x-backward forms u, w, omega_x, omega_z from them, kspec_kernel)
+    double om[2][R], v[2][R], d[2][R];
     st.template commit<0>(om);
     if (has_next) st.template prefetch_at<0>(omega, next_line0);
     fresh();
-    d1_apply_to<R, 2, XM>(t, om, d, xl, lane);  // D1 omega (mean line: dU/dy)
+    d1_apply_to<R, 2, XM>(t, om, d, xl, lane);
     double dU0 = 0.0, dUN = 0.0;
     if (a.mean_diag && is_mean) {
       dU0 = row_value<R, XM>(d[0], 0, lane);
       dUN = row_value<R, XM>(d[0], N - 1, lane);
     }
+    st.store(static_cast<T2*>(a.out[2]), d[0], d[1]);
     st.template commit<2>(v);
     if (has_next) st.template prefetch_at<2>(vin, next_line0);
-    {
-      double ph[2][R];
-      st.template commit<1>(ph);
-      if (has_next) st.template prefetch_at<1>(phi, next_line0);
-      // D2 v = phi + k2 v (Helmholtz identity); wx = Dw - i be v, wz = i al v - Du
-      // (convolution_kernels.cu:46-53), u, w from (nonLinear_kernels.cu:55-72)
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const double DDr = nz * ph[0][r] + k2 * v[0][r], DDi = nz * ph[1][r] + k2 * v[1][r];
-        const double br = (be * DDr + al * d[0][r]) * inv_k2, bi = (be * DDi + al * d[1][r]) * inv_k2;
-        x[0][r] = -bi + be * v[1][r];
-        x[1][r] = br - be * v[0][r];
-      }
-      st.store(static_cast<T2*>(a.out[3]), x[0], x[1]);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const double DDr = nz * ph[0][r] + k2 * v[0][r], DDi = nz * ph[1][r] + k2 * v[1][r];
-        const double ar = (al * DDr - be * d[0][r]) * inv_k2, ai = (al * DDi - be * d[1][r]) * inv_k2;
-        x[0][r] = -al * v[1][r] + ai - mf * d[0][r];
-        x[1][r] = al * v[0][r] - ar;
-      }
-      st.store(static_cast<T2*>(a.out[5]), x[0], x[1]);
-    }
     fresh();
     d1_apply_to<R, 2, XM>(t, v, d, xl, lane);  // D1 v
     auto vel_u = [&](int r, double& re, double& im) {
@@ -1239,13 +1176,7 @@ __global__ void __launch_bounds__(W * 64) kspec_out_kernel(YTab tg, SpecArgs a) 
       }
       __syncthreads();
     }
-#pragma unroll
-    for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
-    st.store(static_cast<T2*>(a.out[0]), x[0], x[1]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
-    st.store(static_cast<T2*>(a.out[2]), x[0], x[1]);
-    if (a.out[4] != a.omega) st.store(static_cast<T2*>(a.out[4]), om[0], om[1], 1.0 - mf);
+    st.store(static_cast<T2*>(a.out[0]), d[0], d[1]);
     if (a.mean_diag && is_mean) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {

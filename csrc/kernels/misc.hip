@@ -144,16 +144,26 @@ __global__ void __launch_bounds__(256) spectra_kernel(SpectraArgs a) {
   const int ig = a.kx0 + ikx;
   const int kx = ig <= a.Kx ? ig : ig - a.nkx;
   const int akx = kx < 0 ? -kx : kx;
-  const T2* f[3] = {static_cast<const T2*>(a.u), static_cast<const T2*>(a.v), static_cast<const T2*>(a.w)};
+  const T2* dv = static_cast<const T2*>(a.dv);
+  const T2* vv = static_cast<const T2*>(a.v);
+  const T2* om = static_cast<const T2*>(a.om);
+  const double al = a.ax * kx;
   double sx[3] = {0.0, 0.0, 0.0};
   for (int kl = threadIdx.x; kl < a.nkz_loc; kl += blockDim.x) {
     const int kz = a.kz0 + kl;
     const size_t idx = spec_index(a.kzb, a.nkx_loc, a.nkzs, j, ikx, kl);
     const double wgt = (kx == 0 && kz == 0) ? 0.0 : (kz == 0 ? 1.0 : 2.0);
+    const double be = a.az * kz, k2 = al * al + be * be, r = k2 > 0.0 ? 1.0 / k2 : 0.0;
+    const T2 d = dv[idx], o = om[idx];
+    // |u|^2 = |al D1v - be om|^2 / k2^2, |w|^2 = |be D1v + al om|^2 / k2^2 (nonLinear_kernels.cu:55-72)
+    const double ur = (al * d.x - be * o.x) * r, ui = (al * d.y - be * o.y) * r;
+    const double wr = (be * d.x + al * o.x) * r, wi = (be * d.y + al * o.y) * r;
+    const T2 c1 = vv[idx];
+    const double en[3] = {ur * ur + ui * ui, static_cast<double>(c1.x) * c1.x + static_cast<double>(c1.y) * c1.y,
+                          wr * wr + wi * wi};
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      const T2 c = f[q][idx];
-      const double e = static_cast<double>(c.x) * c.x + static_cast<double>(c.y) * c.y;
+      const double e = en[q];
       sx[q] += wgt * e;
       atomicAdd(&a.ekz[(static_cast<size_t>(q) * a.nplanes + pl) * a.nkz + kz], wgt * e);
       if (pl == 0 && a.map) a.map[(static_cast<size_t>(q) * a.nkx + ig) * a.nkz + kz] = (kx == 0 && kz == 0) ? 0.0 : e;

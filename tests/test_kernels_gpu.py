@@ -159,7 +159,8 @@ def test_xfft_blocked_layout(native, NX, nkz, dtype, nt, variant):
         buf[f * fstride + idx] = s[f]
     bt = torch.tensor(buf, dtype=dtype, device=DEV)
     phys = native.xfft_backward_blocked(bt, F, rows, y0, ny, NX, Kx, nkz, nt, 4)
-    assert native.xfft_last_variant() == "xfft_backward_kernel" + variant, native.xfft_last_variant()
+    bvariant = variant[:-1] + ", false>"  # (the backward's combine argument)
+    assert native.xfft_last_variant() == "xfft_backward_kernel" + bvariant, native.xfft_last_variant()
     pos = np.where(np.arange(nkx) <= Kx, np.arange(nkx), NX - (nkx - np.arange(nkx)))
     full = np.zeros((F, ny, NX, nkz), complex)
     full[:, :, pos, :] = s[:, y0:y0 + ny]
@@ -176,6 +177,79 @@ def test_xfft_blocked_layout(native, NX, nkz, dtype, nt, variant):
         g = got[f * fstride + idx]
         assert rel(g[y0:y0 + ny] / NX, s[f, y0:y0 + ny]) < tol, f
         assert np.all(g[:y0] == 7.0 + 7.0j) and np.all(g[y0 + ny:] == 7.0 + 7.0j), f
+
+
+def _combine_ref(s, NX, Kx, ax, az, kz0):
+    """The six physical-stage fields u, v, w, omega_x, omega_y, omega_z from the five K-SPEC outputs
+    (D1 v, v, D1 omega, omega, phi) [5, ny, nkx, nkz], x-backward transformed (fft_impl.hpp cmb_pair)."""
+    nkx, nkz = s.shape[2], s.shape[3]
+    kxs = np.where(np.arange(nkx) <= Kx, np.arange(nkx), np.arange(nkx) - nkx)
+    al = (ax * kxs)[None, :, None]
+    be = (az * (kz0 + np.arange(nkz)))[None, None, :]
+    k2 = al * al + be * be
+    r = np.where(k2 > 0, 1.0 / np.where(k2 > 0, k2, 1.0), 0.0)
+    dv, v, dom, om, phi = s
+    mean = (k2 == 0).astype(float)
+    u = 1j * (al * dv - be * om) * r + mean * om.real
+    w = 1j * (be * dv + al * om) * r
+    wx = 1j * (be * phi + al * dom) * r
+    wz = 1j * (be * dom - al * phi) * r - mean * dom.real
+    wy = om * (1.0 - mean)
+    six = np.stack([u, v, w, wx, wy, wz])
+    pos = np.where(np.arange(nkx) <= Kx, np.arange(nkx), NX - (nkx - np.arange(nkx)))
+    full = np.zeros((6, s.shape[1], NX, nkz), complex)
+    full[:, :, pos, :] = six
+    return np.fft.ifft(full, axis=2) * NX
+
+
+# Combine mode (the solver's x-backward): K-SPEC stores D1 v, v, D1 omega next to the omega and phi
+# states, and the gather forms u, v, w, omega_x, omega_y, omega_z per element.  The blocked cases
+# run the headline instantiation (1024-point fp32 plane tiles, 16-byte accesses) and the fp64 /
+# odd-nkz / other-length variants; the plain cases the [y][kx][kz] layout of P > 1 (kz0 > 0: a
+# pencil row's kz range).
+@pytest.mark.parametrize("NX,nkz,dtype,nt,variant", [
+    (1024, 342, torch.complex64, 1, "<1024, float, false, 1, 0, 2, 2, true>"),
+    (1024, 341, torch.complex64, 0, "<1024, float, false, 1, 0, 1, 2, true>"),
+    (1024, 342, torch.complex128, 1, "<1024, double, false, 0, 0, 1, 1, true>"),
+    (512, 86, torch.complex64, 0, "<512, float, false, 1, 0, 2, 2, true>"),
+    (2048, 20, torch.complex64, 1, "<2048, float, false, 0, 0, 2, 1, true>"),
+    (768, 50, torch.complex128, 0, "<768, double, false, 0, 0, 1, 1, true>"),
+])
+def test_xfft_combine_blocked(native, NX, nkz, dtype, nt, variant):
+    rng = np.random.default_rng(NX + nkz + 1)
+    Kx = NX // 3
+    nkx = 2 * Kx + 1
+    rows, y0, ny = 13, 3, 6
+    ax, az = 0.5, 2.0
+    s = rng.standard_normal((5, rows, nkx, nkz)) + 1j * rng.standard_normal((5, rows, nkx, nkz))
+    idx, fstride = _blocked_index(rows, nkx, nkz)
+    buf = np.zeros(5 * fstride, complex)
+    for f in range(5):
+        buf[f * fstride + idx] = s[f]
+    bt = torch.tensor(buf, dtype=dtype, device=DEV)
+    phys = native.xfft_backward_blocked(bt, 5, rows, y0, ny, NX, Kx, nkz, nt, -1, combine=1, ax=ax, az=az)
+    assert native.xfft_last_variant() == "xfft_backward_kernel" + variant, native.xfft_last_variant()
+    ref = _combine_ref(s[:, y0:y0 + ny], NX, Kx, ax, az, 0)
+    tol = 1e-12 if dtype == torch.complex128 else 3e-6
+    assert rel(phys.cpu().numpy(), ref) < tol
+
+
+@pytest.mark.parametrize("NX,nkz,kz0,dtype", [(1024, 20, 0, torch.complex64), (1024, 21, 5, torch.complex64),
+                                              (128, 43, 0, torch.complex128), (96, 13, 3, torch.complex64),
+                                              (2048, 9, 0, torch.complex128), (384, 20, 0, torch.complex64)])
+def test_xfft_combine(native, NX, nkz, kz0, dtype):
+    rng = np.random.default_rng(NX + kz0)
+    Kx = NX // 3
+    nkx = 2 * Kx + 1
+    ny = 5
+    ax, az = 1.0, 2.0
+    s = rng.standard_normal((5, ny, nkx, nkz)) + 1j * rng.standard_normal((5, ny, nkx, nkz))
+    st = torch.tensor(s, dtype=dtype, device=DEV)
+    phys = native.xfft_backward(st, NX, Kx, combine=1, ax=ax, az=az, kz0=kz0)
+    assert native.xfft_last_variant().endswith(", true>"), native.xfft_last_variant()
+    ref = _combine_ref(s, NX, Kx, ax, az, kz0)
+    tol = 1e-12 if dtype == torch.complex128 else 3e-6
+    assert rel(phys.cpu().numpy(), ref) < tol
 
 
 @pytest.mark.parametrize("NX,Nzp,dtype", [(32, 32, torch.complex128), (64, 128, torch.complex64),

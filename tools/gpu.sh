@@ -7,7 +7,8 @@
 #   tests            full GPU test suite          (PYTEST_K="not slow" selects by -k, PYTEST_ARGS adds files)
 #   smoke            __graft_entry__.smoke()
 #   bench            bench.py $BENCH_ARGS         (default: the headline grid)
-#   prof             rocprofv3 --kernel-trace --stats of a short bench.py $BENCH_ARGS
+#   prof             rocprofv3 --kernel-trace --stats of a short bench.py $BENCH_ARGS (+ gaps, graph dot)
+#   fcprof           the same with CHANNEL_FORCE_COMM=1 (the P > 1 per-rank pipeline on one GPU)
 #   pmc              PMC counter passes (one rocprofv3 run per counter group) of one bench step
 #   counters         rocprofv3 -L (available PMC counters) -> <TAG>_counter_names.txt
 #   configs          bench.py on every BASELINE config that fits one GPU
@@ -42,9 +43,20 @@ for step in "$@"; do
       timeout -k 10 400 python bench.py $BENCH_ARGS > $log 2>&1 || fail bench $log
       tail -n 1 $log ;;
     prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof -o run --output-format csv \
-        -- python3 bench.py --steps 3 --warmup 1 $BENCH_ARGS > $log 2>&1 || fail prof $log
-      python3 tools/kstats.py "$(find gpurun_out/${tag}_prof -name '*kernel_stats.csv' | head -n 1)" 10 ;;
+      CHANNEL_GRAPH_DOT=gpurun_out/${tag}_graph timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_prof \
+        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 $BENCH_ARGS > $log 2>&1 || fail prof $log
+      python3 tools/kstats.py "$(find gpurun_out/${tag}_prof -name '*kernel_stats.csv' | head -n 1)" 10
+      python3 tools/trace_gaps.py "$(find gpurun_out/${tag}_prof -name '*kernel_trace.csv' | head -n 1)" > gpurun_out/${tag}_gaps.txt
+      tail -n 1 gpurun_out/${tag}_gaps.txt ;;
+    fcprof)
+      # the P > 1 per-rank pipeline on a 1-rank RCCL communicator: kernel trace, inter-kernel gaps,
+      # step-graph topology (dot) next to the P = 1 one
+      CHANNEL_FORCE_COMM=1 CHANNEL_GRAPH_DOT=gpurun_out/${tag}_graph_fc timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+        -d gpurun_out/${tag}_fcprof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 $BENCH_ARGS \
+        > $log 2>&1 || fail fcprof $log
+      python3 tools/kstats.py "$(find gpurun_out/${tag}_fcprof -name '*kernel_stats.csv' | head -n 1)" 10
+      python3 tools/trace_gaps.py "$(find gpurun_out/${tag}_fcprof -name '*kernel_trace.csv' | head -n 1)" > gpurun_out/${tag}_fc_gaps.txt
+      tail -n 1 gpurun_out/${tag}_fc_gaps.txt ;;
     pmc)
       i=0
       for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
