@@ -191,6 +191,7 @@ PYBIND11_MODULE(_core, m) {
       .def("kblocks", &Solver::kblocks)
       .def("bwd_blocks_issued", &Solver::bwd_blocks_issued)
       .def("spec_kzb", &Solver::spec_kzb)
+      .def("combine", &Solver::combine)
       .def("mean_profile", [](Solver& s) { return vec(s.mean_profile()); })
       .def("health", &Solver::health)
       .def("time", &Solver::time)

@@ -23,6 +23,36 @@ Split Split::balanced(int n, int parts) {
   return s;
 }
 
+// n items in groups of a (the last group may be partial) over `parts`: whole groups balanced, the
+// extra groups on the LAST parts, so the partial group lands on a part with an extra group (NY =
+// 385 in groups of 8 over 8 parts: 48 x 7 + 49, the balanced split's maximum).  Every part gets at
+// least one group (the caller checks ceil(n / a) >= parts).
+Split Split::aligned(int n, int parts, int a) {
+  const int ng = (n + a - 1) / a;
+  CH_CHECK(parts >= 1 && ng >= parts, "cannot split " << ng << " groups of " << a << " over " << parts << " parts");
+  Split s;
+  s.n = n;
+  s.parts = parts;
+  s.start.resize(parts);
+  s.count.resize(parts);
+  const int base = ng / parts, rem = ng % parts;
+  int off = 0;
+  for (int p = 0; p < parts; ++p) {
+    const int g = base + (p >= parts - rem ? 1 : 0);
+    s.start[p] = off;
+    s.count[p] = std::min(g * a, n - off);
+    off += s.count[p];
+  }
+  return s;
+}
+
+void Plan::align_y(int a) {
+  y_split = Split::aligned(NY, Pc, a);
+  ny_loc = y_split.count[pcol];
+  y0 = y_split.start[pcol];
+  yalign = a;
+}
+
 int Split::owner(int idx) const {
   for (int p = parts - 1; p >= 0; --p)
     if (idx >= start[p]) return p;

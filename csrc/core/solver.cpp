@@ -159,7 +159,42 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
   }
   tw_x_.build(plan_.NX, fp64_);
   tw_z_.build(plan_.Nzp, fp64_);
+  choose_layout();
   alloc();
+}
+
+// Spectral layout: blocked [y/8][line/8][y%8][line%8] (kzb_ = 8, spec_index) where it measured
+// faster: R = 7, 8 (1024x385x1024: 39.5 -> 35.8 ms/step at one rank); the plain layout stays at
+// R = 5 (512x257x512: 7.37 vs 7.63) and R = 10 (2048x633x2048: 315 vs 323; profiles/r04/
+// ab_layout_grids.txt).  CHANNEL_SPEC_KZB=0/1 forces it off/on (A/B).  At P > 1 the exchange blocks
+// are row ranges of every line, so the y split is taken in whole 8-plane tiles (Plan::align_y: NY =
+// 385 over 8 ranks is 48 x 7 + 49, the balanced split's maximum) and every block stays contiguous;
+// the x kernels address the exchange segments in the same tiles (XArgs::segblk).  The same choice
+// on every rank (a function of the grid, the precision and the environment).
+void Solver::choose_layout() {
+  const Plan& p = plan_;
+  // The physical-stage fields: at P > 1 K-SPEC writes D1 v, v, D1 omega and the x-backward forms
+  // u, w, omega_x, omega_z from them (combine): the backward exchange moves 5 fields instead of 6.
+  // At one rank (no exchange, also the 1-rank RCCL communicator) K-SPEC writes the six fields: the
+  // same K-SPEC time (4.15 ms per substep with 7 or 9 stores) and one-input x-backward tiles of
+  // whole 128-B lines, 61 vs 71 us per 6-plane chunk (profiles/r06/).  CHANNEL_COMBINE=0/1 forces it.
+  combine_ = comm_ && p.P > 1;
+  if (const char* e = std::getenv("CHANNEL_COMBINE")) combine_ = std::atoi(e) != 0;
+  kzb_ = (p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
+  if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = std::atoi(e) != 0 ? kSpecKzBlock : 0;
+  // (the x transforms address a blocked field with 32-bit byte offsets: above 4 GiB per field the
+  // plain layout is used, also when CHANNEL_SPEC_KZB=1 asks for the blocked one)
+  if (kzb_ && static_cast<unsigned long long>(spec_rows(kSpecKzBlock, p.NY)) * p.nkx_loc *
+                      ((p.nkz_loc + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock) * (fp64_ ? 16 : 8) >= (1ull << 32)) {
+    if (std::getenv("CHANNEL_SPEC_KZB")) std::fprintf(stderr, "[channel] CHANNEL_SPEC_KZB ignored: a blocked field would exceed 4 GiB\n");
+    kzb_ = 0;
+  }
+  if (comm_ && kzb_) {
+    // every column-group rank needs a whole tile of planes; the round-1 per-field pencil exchange
+    // (A/B) keeps the plain layout
+    if ((p.NY + kSpecYBlock - 1) / kSpecYBlock < p.Pc || std::getenv("CHANNEL_PENCIL_UNCHUNKED")) kzb_ = 0;
+    else plan_.align_y(kSpecYBlock);
+  }
 }
 
 Solver::~Solver() {
@@ -183,19 +218,7 @@ Solver::~Solver() {
 
 void Solver::alloc() {
   const Plan& p = plan_;
-  // blocked spectral layout at one rank (CHANNEL_SPEC_KZB=0/1 forces it off/on, A/B); P > 1 keeps
-  // [y][line]: its exchange blocks are row ranges of every line.  Default on where it measured
-  // faster: R = 7, 8 (1024x385x1024: 39.5 -> 35.8 ms/step); the plain layout stays at R = 5
-  // (512x257x512: 7.37 vs 7.63) and R = 10 (2048x633x2048: 315 vs 323; profiles/r04/ab_layout_grids.txt)
-  kzb_ = (!comm_ && p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
-  if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = (!comm_ && std::atoi(e) != 0) ? kSpecKzBlock : 0;
-  // (the x transforms address a blocked field with 32-bit byte offsets: above 4 GiB per field the
-  // plain layout is used, also when CHANNEL_SPEC_KZB=1 asks for the blocked one)
-  if (kzb_ && static_cast<unsigned long long>(spec_rows(kSpecKzBlock, p.NY)) * p.nkx_loc *
-                      ((p.nkz_loc + kSpecKzBlock - 1) / kSpecKzBlock * kSpecKzBlock) * (fp64_ ? 16 : 8) >= (1ull << 32)) {
-    if (std::getenv("CHANNEL_SPEC_KZB")) std::fprintf(stderr, "[channel] CHANNEL_SPEC_KZB ignored: a blocked field would exceed 4 GiB\n");
-    kzb_ = 0;
-  }
+  // (kzb_: choose_layout)
   nkzs_ = kzb_ ? (p.nkz_loc + kzb_ - 1) / kzb_ * kzb_ : p.nkz_loc;
   canon_ = p.spec_elems();
   spec_ = static_cast<size_t>(spec_rows(kzb_, p.NY)) * p.nkx_loc * nkzs_;
@@ -222,7 +245,9 @@ void Solver::alloc() {
     kb_start_ = kb.start;
     kb_cnt_ = kb.count;
     kb_off_.assign(nkb_, 0);
-    for (int b = 1; b < nkb_; ++b) kb_off_[b] = kb_off_[b - 1] + static_cast<size_t>(p.NY) * kb_cnt_[b - 1] * p.nkz_loc;
+    // (each block a [y][lines_b] region, blocked like the whole field when kzb_: spec_index)
+    for (int b = 1; b < nkb_; ++b)
+      kb_off_[b] = kb_off_[b - 1] + static_cast<size_t>(spec_rows(kzb_, p.NY)) * kb_cnt_[b - 1] * nkzs_;
     ev_kb_.resize(nkb_);
     for (auto& e : ev_kb_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ev_fb_.resize(nkb_);
@@ -231,7 +256,9 @@ void Solver::alloc() {
     // CHANNEL_FWD_SPLIT=0: the whole forward exchange completes before K-SPEC (A/B)
     if (const char* e = std::getenv("CHANNEL_FWD_SPLIT")) fwd_split_ = std::atoi(e) != 0;
   }
-  xstride_ = static_cast<size_t>(p.ny_loc) * p.nkx * p.nkz_loc;
+  // exchange receive buffer per field: segments [src column][y_loc][kx of the segment][kz] (blocked
+  // like the spectral fields when kzb_: rows padded to whole 8-plane tiles, kz lines to nkzs_)
+  xstride_ = static_cast<size_t>(spec_rows(kzb_, p.ny_loc)) * p.nkx * nkzs_;
   zstride_ = p.pencil() ? p.zrow_elems() : 0;
   // state_ = phi, R_phi, R_omega; the omega state is out_ field 4 (it IS the omega_y output of
   // K-SPEC, which then stores one field less per substep; the x transform zeroes its mean line)
@@ -291,6 +318,8 @@ void Solver::alloc() {
   if (const char* ps = std::getenv("CHANNEL_PSTREAMS")) pstreams_ = std::max(1, std::min(2, std::atoi(ps)));
   ychunk_p_ = std::min(64, pstreams_ >= 2 ? planes_in(104) : planes_in(144));
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
+  // blocked layout at P > 1: exchange chunks of whole 8-plane tiles (contiguous blocks)
+  if (comm_ && kzb_ && ychunk_p_ > 0) ychunk_p_ = std::max(kSpecYBlock, ychunk_p_ / kSpecYBlock * kSpecYBlock);
   // CHANNEL_A2A_SELF = direct (default: the x transforms access the own block in place) | copy
   // (D2D copy inside the exchange) | rccl (through ncclSend/ncclRecv; RcclComm reads it too)
   if (const char* sm = std::getenv("CHANNEL_A2A_SELF")) self_direct_ = std::string(sm) == "direct";
@@ -381,10 +410,11 @@ void* Solver::field_ptr(int f) const {
 // Input j of the x-backward's combine mode (XArgs::combine): 0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi
 // -- what K-SPEC leaves for the physical-space stage; the backward exchange of P > 1 moves these
 // five fields (the forward one the three H fields)
+// (six-output mode: the six fields u, v, w, omega_x, omega_y (the omega state), omega_z)
 void* Solver::in_field(int j) const {
-  static const Field kIn[kBwdFields] = {OUT0, OUT1, OUT2, OMEGA, PHI};
-  CH_CHECK(j >= 0 && j < kBwdFields, "bad combine input " << j);
-  return field_ptr(kIn[j]);
+  static const Field kIn[5] = {OUT0, OUT1, OUT2, OMEGA, PHI};
+  CH_CHECK(j >= 0 && j < bwd_fields(), "bad backward field " << j);
+  return combine_ ? field_ptr(kIn[j]) : field_ptr(OUT0 + j);
 }
 
 int Solver::kb_gstart(int c, int b) const {
@@ -394,12 +424,9 @@ int Solver::kb_gcount(int c, int b) const { return Split::balanced(plan_.kx_spli
 size_t Solver::kb_index(int y, int ikx, int kz) const {
   int b = nkb_ - 1;
   while (b > 0 && ikx < kb_start_[b]) --b;
-  return kb_off_[b] + (static_cast<size_t>(y) * kb_cnt_[b] + (ikx - kb_start_[b])) * plan_.nkz_loc + kz;
+  return kb_off_[b] + spec_index(kzb_, kb_cnt_[b], nkzs_, y, ikx - kb_start_[b], kz);
 }
-size_t Solver::dev_index(int y, int ikx, int kz) const {
-  if (kzb_) return spec_index(kzb_, plan_.nkx_loc, nkzs_, y, ikx, kz);
-  return kb_index(y, ikx, kz);
-}
+size_t Solver::dev_index(int y, int ikx, int kz) const { return kb_index(y, ikx, kz); }
 
 // ---- state ------------------------------------------------------------------------------------
 void Solver::set_state(const std::complex<double>* phi, const std::complex<double>* omega, const double* U) {
@@ -609,6 +636,7 @@ void Solver::kspec(int mode, int n, bool stats) {
   a.health = cfg_.health_check ? d_health_ : nullptr;
   a.prof = kprof_on_ ? d_kprof_ : nullptr;
   a.lds_poison = lds_poison_enabled() ? 1 : 0;
+  a.out6 = combine_ ? 0 : 1;
   if (stats) HIP_CHECK(hipMemsetAsync(d_stats_, 0, 4 * p.NY * sizeof(double), s_comp_));
   ev(0, false);
   // (measured r2s: splitting this fused pass into an advance kernel and a prepare kernel frees no
@@ -773,8 +801,10 @@ void Solver::transforms(int n, bool /*stats*/) {
   xa.nkz = p.nkz;
   xa.ny = p.ny_loc;
   xa.field_stride_phys = static_cast<long long>(physn_);
-  // u, v, w, omega_x, omega_y, omega_z formed per element from the five K-SPEC outputs (combine)
-  xa.combine = 1;
+  // u, v, w, omega_x, omega_y, omega_z: read (omega_y's source is the omega state, whose mean line
+  // holds U: read as 0) or formed per element from the five combine-mode outputs
+  xa.combine = combine_ ? 1 : 0;
+  xa.zero_mean_field = combine_ ? -1 : 4;
   xa.ax = p.ax;
   xa.az = p.az;
   xa.kz_glob0 = p.kz0;
@@ -822,7 +852,8 @@ void Solver::transforms(int n, bool /*stats*/) {
     src.nsrc = 1;
     src.kx_start[0] = 0;
     src.kx_start[1] = p.nkx;
-    for (int j = 0; j < kBwdFields; ++j) src.fld[j] = in_field(j);
+    if (combine_)
+      for (int j = 0; j < kCmbIn; ++j) src.fld[j] = in_field(j);
     xa.nfields = 6;
     xa.field_stride_spec = static_cast<long long>(spec_);
     XDst dst;
@@ -857,7 +888,8 @@ void Solver::transforms(int n, bool /*stats*/) {
         if (kzb_) xc.spec_y0 = y0;
         XSrc sc = src;
         sc.base = static_cast<char*>(out_) + so;
-        for (int j = 0; j < kBwdFields; ++j) sc.fld[j] = static_cast<const char*>(src.fld[j]) + so;
+        if (combine_)
+          for (int j = 0; j < kCmbIn; ++j) sc.fld[j] = static_cast<const char*>(src.fld[j]) + so;
         xc.nfields = 6;
         ev(1, false, cs);
         xfft_backward(xc, sc, ph, tw_x_, fp64_, cs);
@@ -941,7 +973,7 @@ void Solver::transforms(int n, bool /*stats*/) {
   auto fld = [&](void* base, size_t stride, int f) { return static_cast<char*>(base) + static_cast<size_t>(f) * stride * esz_; };
   HIP_CHECK(hipEventRecord(ev_spec_, s_comp_));
   HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
-  for (int f = 0; f < kBwdFields; ++f) {
+  for (int f = 0; f < bwd_fields(); ++f) {
     ev(4, false, s_comm_);
     a2a_spec(in_field(f), fld(xbuf_, xstride_, f), true);
     ev(4, true, s_comm_);
@@ -951,7 +983,10 @@ void Solver::transforms(int n, bool /*stats*/) {
   ev(1, false);
   {
     XSrc sf = src;
-    for (int j = 0; j < kBwdFields; ++j) sf.fld[j] = fld(xbuf_, xstride_, j);
+    if (combine_)
+      for (int j = 0; j < kCmbIn; ++j) sf.fld[j] = fld(xbuf_, xstride_, j);
+    else
+      xa.zero_mean_field = 4;
     xfft_backward(xa, sf, phys_, tw_x_, fp64_, s_comp_);
   }
   if (pen) {  // ship the x-blocks of the six fields to the row group
@@ -1031,6 +1066,10 @@ void Solver::a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bh
   std::vector<A2ABlock> ops;
   ops.reserve(static_cast<size_t>(nf) * (bhi - blo));
   if (to_phys) bwd_blocks_issued_ += bhi - blo;  // (host-side count of issued backward block exchanges)
+  // blocked layout (kzb_): rows go in whole 8-plane tiles (r0 and every rank's first row are tile
+  // aligned; a rank's last tile may be partial and is sent whole: padding rows of the fields)
+  auto rows_pad = [&](size_t n) { return kzb_ ? (n + kSpecYBlock - 1) / kSpecYBlock * kSpecYBlock : n; };
+  const size_t ny_pad = rows_pad(static_cast<size_t>(p.ny_loc));
   for (int f = 0; f < nf; ++f)
     for (int b = blo; b < bhi; ++b) {
       ops.emplace_back();
@@ -1041,15 +1080,15 @@ void Solver::a2a_slab_rows(int r0, int nr, bool to_phys, int nf, int blo, int bh
       o.roff.assign(P, 0);
       char* spec = static_cast<char*>(to_phys ? in_field(f) : field_ptr(OUT0 + f));
       char* xb = static_cast<char*>(xbuf_) + static_cast<size_t>(f) * xstride_ * esz_;
-      const size_t lines_b = static_cast<size_t>(kb_cnt_[b]) * p.nkz_loc;
+      const size_t lines_b = static_cast<size_t>(kb_cnt_[b]) * nkzs_;
       for (int c = 0; c < P; ++c) {
         if (self_direct_ && c == p.pcol) continue;  // read/written in place by the x transforms
-        const size_t nr_c = static_cast<size_t>(std::max(0, std::min(nr, p.y_split.count[c] - r0)));
+        const size_t nr_c = rows_pad(static_cast<size_t>(std::max(0, std::min(nr, p.y_split.count[c] - r0))));
         const size_t yo = (kb_off_[b] + (static_cast<size_t>(p.y_split.start[c]) + r0) * lines_b) * esz_;
         const size_t yc = nr_c * lines_b * esz_;
         const size_t gs = static_cast<size_t>(kb_gstart(c, b)), gc = static_cast<size_t>(kb_gcount(c, b));
-        const size_t xo = (static_cast<size_t>(p.ny_loc) * gs + static_cast<size_t>(r0) * gc) * p.nkz_loc * esz_;
-        const size_t xc = nr_me * gc * p.nkz_loc * esz_;
+        const size_t xo = (ny_pad * gs + static_cast<size_t>(r0) * gc) * nkzs_ * esz_;
+        const size_t xc = rows_pad(nr_me) * gc * nkzs_ * esz_;
         if (to_phys) {
           o.soff[c] = yc ? yo : 0;
           o.scount[c] = yc;
@@ -1090,7 +1129,10 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   }
   XArgs xa = xa0;
   xa.nkz = p.nkz_loc;
+  xa.nkzs = nkzs_;
+  xa.segblk = kzb_ ? 1 : 0;
   xa.field_stride_spec = static_cast<long long>(xstride_);
+  const long long ny_pad = spec_rows(kzb_, p.ny_loc);
   // exchange segments: block b of rank c is segment c * nkb_ + b (global kx order)
   const int NB = nkb_, NS = P * NB;
   CH_CHECK(NS <= kMaxSeg, "at most " << kMaxSeg << " exchange segments");
@@ -1112,10 +1154,11 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
   }
   // combine inputs: received blocks in the exchange buffer (five fields), own blocks in place
-  for (int j = 0; j < kBwdFields; ++j) {
-    src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
-    if (self_direct_) src.self_fld[j] = in_field(j);
-  }
+  if (combine_)
+    for (int j = 0; j < kCmbIn; ++j) {
+      src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
+      if (self_direct_) src.self_fld[j] = in_field(j);
+    }
 
   roctxRangePushA("xzx_slab_chunked");
   // K-SPEC / exchange overlap: blocks 0 .. NB-2 of the previous substep's K-SPEC go out whole as
@@ -1133,7 +1176,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
       ev(4, false, s_comm_);
-      a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
+      a2a_slab_rows(0, maxrows, true, bwd_fields(), b, b + 1);
       ev(4, true, s_comm_);
     }
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
@@ -1143,7 +1186,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   }
   auto backward = [&](int k) {
     ev(4, false, s_comm_);
-    a2a_slab_rows(k * ch, ch, true, kBwdFields, bchunk, NB);
+    a2a_slab_rows(k * ch, ch, true, bwd_fields(), bchunk, NB);
     ev(4, true, s_comm_);
     HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
   };
@@ -1173,11 +1216,11 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
       for (int c = 0; c < P; ++c)
         for (int b = 0; b < NB; ++b)
           src.off[c * NB + b] = dst.off[c * NB + b] =
-              (static_cast<long long>(p.ny_loc) * kb_gstart(c, b) + static_cast<long long>(y0) * kb_gcount(c, b)) * p.nkz_loc;
+              (ny_pad * kb_gstart(c, b) + static_cast<long long>(y0) * kb_gcount(c, b)) * nkzs_;
       if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields (block b)
         for (int b = 0; b < NB; ++b)
           src.off[p.rank * NB + b] = dst.off[p.rank * NB + b] =
-              static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * p.nkz_loc;
+              static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * nkzs_;
       XArgs xc = xa;
       xc.ny = ny;
       xc.nfields = 6;
@@ -1304,7 +1347,10 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
   enum { E_A = 0, E_XB, E_B, E_Z, E_BF, E_XF };
   XArgs xa = xa0;
   xa.nkz = p.nkz_loc;
+  xa.nkzs = nkzs_;
+  xa.segblk = kzb_ ? 1 : 0;
   xa.field_stride_spec = static_cast<long long>(xstride_);
+  const long long ny_pad = spec_rows(kzb_, p.ny_loc);
   xa.npseg = Pr;
   for (int r = 0; r < Pr; ++r) xa.x_start[r] = p.x_split.start[r];
   xa.x_start[Pr] = p.NX;
@@ -1329,10 +1375,11 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     CH_CHECK(spec_ < (1ull << 32), "spectral field exceeds 32-bit element offsets");
   }
   // combine inputs: received blocks in the exchange buffer (five fields), own blocks in place
-  for (int j = 0; j < kBwdFields; ++j) {
-    src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
-    if (self_direct_) src.self_fld[j] = in_field(j);
-  }
+  if (combine_)
+    for (int j = 0; j < kCmbIn; ++j) {
+      src.fld[j] = static_cast<const char*>(xbuf_) + static_cast<size_t>(j) * xstride_ * esz_;
+      if (self_direct_) src.self_fld[j] = in_field(j);
+    }
   ZArgs za = za0;
   za.NX = p.nx_loc;
   za.field_stride = static_cast<long long>(zstride_);
@@ -1348,12 +1395,11 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
       x.poff[r] = (static_cast<long long>(p.ny_loc) * p.x_split.start[r] + y0 * p.x_split.count[r]) * p.nkz_loc;
     for (int c = 0; c < Pc; ++c)
       for (int b = 0; b < NB; ++b)
-        sc.off[c * NB + b] = dc.off[c * NB + b] =
-            (static_cast<long long>(p.ny_loc) * kb_gstart(c, b) + y0 * kb_gcount(c, b)) * p.nkz_loc;
+        sc.off[c * NB + b] = dc.off[c * NB + b] = (ny_pad * kb_gstart(c, b) + y0 * kb_gcount(c, b)) * nkzs_;
     if (self_direct_)
       for (int b = 0; b < NB; ++b)
         sc.off[p.pcol * NB + b] = dc.off[p.pcol * NB + b] =
-            static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * p.nkz_loc;
+            static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * nkzs_;
   };
   auto xbw = [&](int k) {
     if (chunk_rows(k) > 0) {
@@ -1413,7 +1459,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     for (int b = 0; b + 1 < NB; ++b) {
       HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
       ev(4, false, s_comm_);
-      a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
+      a2a_slab_rows(0, maxrows, true, bwd_fields(), b, b + 1);
       ev(4, true, s_comm_);
     }
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[NB - 1], 0));
@@ -1422,7 +1468,7 @@ void Solver::transforms_pencil(int n, const XArgs& xa0, const ZArgs& za0, const 
     HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_spec_, 0));
   }
   for (int t = 0; t < nch + 6; ++t) {
-    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_rows(t * ch, ch, true, kBwdFields, bchunk, NB); });
+    if (t < nch) comm_op(t, -1, E_A, [&] { a2a_slab_rows(t * ch, ch, true, bwd_fields(), bchunk, NB); });
     if (t - 2 >= 0 && t - 2 < nch) comm_op(t - 2, E_XB, E_B, [&] { b2b_pencil_chunk(t - 2, ch, true, 6); });
     if (t - 4 >= 0 && t - 4 < nch) comm_op(t - 4, E_Z, E_BF, [&] { b2b_pencil_chunk(t - 4, ch, false, 3); });
     if (t - 6 >= 0 && t - 6 < nch) comm_op(t - 6, E_XF, -1, [&] { a2a_slab_chunk(t - 6, ch, false, 3); });
@@ -1480,7 +1526,7 @@ void Solver::presend_backward(bool wait_blocks) {
   for (int b = 0; b + 1 < nkb_; ++b) {
     if (wait_blocks) HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_kb_[b], 0));
     ev(4, false, s_comm_);
-    a2a_slab_rows(0, maxrows, true, kBwdFields, b, b + 1);
+    a2a_slab_rows(0, maxrows, true, bwd_fields(), b, b + 1);
     ev(4, true, s_comm_);
   }
   HIP_CHECK(hipEventRecord(ev_fwd_done_, s_comm_));
@@ -1832,7 +1878,7 @@ void Solver::symmetrize() {
     if (has_kz0)  // per kx sub-block: col_loc = [b][y][kx in b], i.e. global kx order again
       for (int b = 0; b < nkb_; ++b)
         kz0_pack(static_cast<char*>(field_ptr(f == 0 ? PHI : OMEGA)) + kb_off_[b] * esz_,
-                 col_loc + (f * loc + static_cast<size_t>(p.NY) * kb_start_[b]) * esz_, p.NY, kb_cnt_[b], p.nkz_loc,
+                 col_loc + (f * loc + static_cast<size_t>(p.NY) * kb_start_[b]) * esz_, p.NY, kb_cnt_[b], nkzs_, kzb_,
                  fp64_, s_comp_);
   }
   HIP_CHECK(hipEventRecord(ev_stats_, s_comp_));
@@ -1843,7 +1889,8 @@ void Solver::symmetrize() {
   if (has_kz0) {
     Kz0SymArgs a;
     a.N = p.NY;
-    a.nkz_loc = p.nkz_loc;
+    a.nkz_loc = nkzs_;  // (the line stride)
+    a.kzb = kzb_;
     a.nkx = p.nkx;
     a.nblk = p.Pc * nkb_;  // gathered blocks (c, b) in global kx order
     for (int c = 0; c < p.Pc; ++c)
@@ -2099,6 +2146,9 @@ Solver::Spectra Solver::spectra() {
   a.om = field_ptr(OMEGA);
   a.ax = p.ax;
   a.az = p.az;
+  a.combine = combine_ ? 1 : 0;
+  a.u = field_ptr(OUT0);
+  a.w = field_ptr(OUT2);
   a.lines = p.nkx_loc * nkzs_;
   a.nkx_loc = p.nkx_loc;
   a.kx0 = p.kx0;
@@ -2120,6 +2170,8 @@ Solver::Spectra Solver::spectra() {
     ab.dv = static_cast<const char*>(a.dv) + off;
     ab.v = static_cast<const char*>(a.v) + off;
     ab.om = static_cast<const char*>(a.om) + off;
+    ab.u = static_cast<const char*>(a.u) + off;
+    ab.w = static_cast<const char*>(a.w) + off;
     ab.lines = kb_cnt_[b] * nkzs_;
     ab.nkx_loc = kb_cnt_[b];
     ab.kx0 = p.kx0 + kb_start_[b];

@@ -111,10 +111,12 @@ struct SpecArgs {
   void* omega = nullptr;  // line (0,0) holds U(y)
   void* Rphi = nullptr;
   void* Romega = nullptr;
-  void* out[6] = {};      // outputs D1 v, v, D1 omega (out[0..2]; they double as the H_x, H_y, H_z
-                          // inputs); out[4] == omega (the state is the omega_y source); out[3] and
-                          // out[5] are unused: the x-backward forms u, w, omega_x, omega_z from
-                          // D1 v, omega, phi, D1 omega (XArgs::combine)
+  void* out[6] = {};      // out6 = 1: u, v, w, omega_x, -, omega_z (out[4] == omega: the state is the
+                          // omega_y source, the x-backward zeroes its mean line); out6 = 0 (the
+                          // combine mode of P > 1): D1 v, v, D1 omega in out[0..2], out[3], out[5]
+                          // unused (XArgs::combine forms u, w, omega_x, omega_z from D1 v, omega,
+                          // phi, D1 omega).  out[0..2] double as the H_x, H_y, H_z inputs.
+  int out6 = 1;
   int store_r = 1;        // 0: skip the R_phi/R_omega stores (last substep: the next one has zeta = 0)
   int lds_poison = 0;     // debug: fill the LDS with NaN before use (CHANNEL_LDS_POISON)
   // diagnostics
@@ -189,6 +191,10 @@ struct XArgs {
   // blocked spectral layout (one rank, one source block; spec_index with kzb = 8): rows spec_y0 ..
   // spec_y0 + ny - 1 of fields of line stride nkzs (lines = nkx * nkzs)
   int kzb = 0, nkzs = 0, spec_y0 = 0;
+  // P > 1: the exchange segments and self blocks hold the blocked layout too (spec_index with
+  // kzb = 8 within each segment: [y/8][line/8][y%8][line%8], line = kx in segment * nkzs + kz;
+  // chunk rows start on 8-plane tiles).  fft_impl.hpp seg_yk / seg_stride
+  int segblk = 0;
   int nt = 0;                        // streaming (non-temporal) spectral accesses (solver default 1;
                                      // CHANNEL_XNT=0 off: 35.0 vs 34.75 ms/step, profiles/r04/ab_xnt.txt)
   // backward only: combine mode -- the six output fields u, v, w, omega_x, omega_y, omega_z are
@@ -245,10 +251,11 @@ void symmetrize_kz0(void* q, int N, int nkx, int nkzs, int Kx, int kzb, bool fp6
 // gathered columns (blocks [c][y][nkx_c] of the ranks of this process row)
 struct Kz0SymArgs {
   int N = 0, nkx_loc = 0, nkz_loc = 0, kx0 = 0, nkx = 0;
+  int kzb = 0;  // spectral layout of q (spec_index; nkz_loc is then the padded line stride nkzs)
   int nblk = 1;
   int kx_start[kMaxSeg + 1] = {0};
 };
-void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp64, hipStream_t s);
+void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, int kzb, bool fp64, hipStream_t s);
 void kz0_symmetrize_dist(void* q, const void* col_all, const Kz0SymArgs& a, bool fp64, hipStream_t s);
 
 // ---- diagnostics ---------------------------------------------------------------------------
@@ -257,6 +264,9 @@ struct SpectraArgs {
   // state; u = i (al D1v - be om)/k2 and w = i (be D1v + al om)/k2 are formed per element
   const void *dv = nullptr, *v = nullptr, *om = nullptr;
   double ax = 1.0, az = 2.0;
+  // combine = 0 (K-SPEC's six-output mode): u and w are stored fields themselves
+  int combine = 1;
+  const void *u = nullptr, *w = nullptr;
   int lines = 0, nkx_loc = 0, kx0 = 0, nkz_loc = 0, kz0 = 0;
   int nkzs = 0, kzb = 0;              // line stride in kz, layout (spec_index)
   int nkx = 0, Kx = 0, nkz = 0;       // global retained counts

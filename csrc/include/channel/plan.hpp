@@ -34,6 +34,8 @@ struct Split {
   int n = 0, parts = 1;
   std::vector<int> start, count;
   static Split balanced(int n, int parts);
+  // groups of a items (the last one may be partial), balanced over the parts (Plan::align_y)
+  static Split aligned(int n, int parts, int a);
   int owner(int idx) const;
   int max_count() const;
 };
@@ -53,7 +55,12 @@ struct Plan {
   int R = 1;                  // rows per lane of the 64-lane y-line solver: 64 * R >= NY
   double ax = 1.0, az = 2.0;  // 2*pi/LX, 2*pi/LZ
 
+  int yalign = 1;             // y split in whole groups of yalign planes (align_y)
+
   static Plan make(const Config& cfg, int P, int rank);
+  // y split in groups of a planes: the blocked spectral layout at P > 1 (Solver) keeps each
+  // rank's y range whole 8-plane tiles, so the exchange blocks stay contiguous
+  void align_y(int a);
 
   bool pencil() const { return Pr > 1; }
   int rank_of(int row, int col) const { return row * Pc + col; }

@@ -127,8 +127,11 @@ class Solver {
   // ---- raw device access (tests / bindings) ----------------------------------------------
   enum Field { PHI = 0, OMEGA, RPHI, ROMEGA, OUT0, OUT1, OUT2, OUT3, OUT4, OUT5 };
   void* field_ptr(int f) const;
-  // input j of the x-backward's combine mode (0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi)
-  static constexpr int kBwdFields = 5;
+  // backward-exchanged field j: the combine mode's inputs (0 D1 v, 1 v, 2 D1 omega, 3 omega, 4 phi)
+  // or the six physical-stage fields (choose_layout)
+  static constexpr int kCmbIn = 5;
+  int bwd_fields() const { return combine_ ? kCmbIn : 6; }
+  bool combine() const { return combine_; }
   void* in_field(int j) const;
   void* phys_ptr() const { return phys_; }
   const YTablesDev& ytables() const { return ytab_; }
@@ -149,6 +152,7 @@ class Solver {
   double max_over_ranks(double v);
 
  private:
+  void choose_layout();
   void alloc();
   void free_all();
   void transforms(int substep, bool stats);
@@ -214,6 +218,7 @@ class Solver {
   // stride nkzs_ padded to a multiple of 8; canon_ = NY * nkx_loc * nkz_loc, the element count of
   // the canonical host layout [y][kx_loc][kz_loc] (set_state / get_state / restart files)
   int kzb_ = 0, nkzs_ = 0;
+  bool combine_ = false;  // K-SPEC's combine-mode outputs + the combining x-backward (choose_layout)
   size_t canon_ = 0;
 
   // device scalars / diagnostics (one allocation)

@@ -106,7 +106,7 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   CH_CHECK(a.ny > 0 && a.nkz > 0, "xfft_backward: empty");
   // the first pass skips the zero band of the 2/3 rule at compile time (wave_pass ZB)
   CH_CHECK(a.Kx == a.NX / 3 && a.nkx == 2 * a.Kx + 1, "xfft_backward: retained kx must be the 2/3 rule's (Kx = NX/3)");
-  CH_CHECK(a.combine || a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
+  CH_CHECK(a.field_stride_spec < (1LL << 32), "xfft_backward: per-field spectral block exceeds 32-bit offsets");
   if (a.combine) {
     for (int j = 0; j < kCmbInputs; ++j)
       CH_CHECK(src.fld[j] && (src.self_seg < 0 || src.self_fld[j]), "xfft_backward: combine mode input field " << j << " missing");

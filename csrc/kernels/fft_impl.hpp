@@ -137,9 +137,12 @@ __device__ __forceinline__ SegPos seg_find_win(const int* start, const long long
 // lookups of the other modes spilled 375-402 SGPRs into VGPR lanes at 1024 points)
 constexpr int kSegOne = 0, kSegWin = 1, kSegFull = 2, kSegRows = 3;
 constexpr int kSegRowsMax = 24;  // rows per thread with a table (longer rows keep the lookups)
-// kSegRows: element offset of row i at y = 0 (off + (i - start) nkz), the y stride of its segment
-// (count nkz), and whether the segment is a self block, for the K rows i = (tid + k NT) / CW of a
-// thread (clamped to the last row like the accesses)
+// kSegRows: element offset of row i at y = 0 (off + (i - start) S), the y stride of its segment
+// (count S), and whether the segment is a self block, for the K rows i = (tid + k NT) / CW of a
+// thread (clamped to the last row like the accesses).  S = nkz for [y][kx][kz] segments; blocked
+// segments (XArgs::segblk: [y/8][line/8][y%8][line%8], line = kx * nkzs + kz) take S = 8 nkzs and
+// the access coordinates (Y, KZ) of seg_yk.
+// x-expanded segments (the pencil's x rows) keep S = nkz.
 template <int K>
 struct SegRows {
   unsigned a[K], b[K];
@@ -156,11 +159,23 @@ struct SegRows {
       if (static_cast<unsigned>(sp.idx - self_seg) < static_cast<unsigned>(nself)) self |= 1u << k;
     }
   }
-  __device__ __forceinline__ unsigned at(int k, int y, int kz) const {
-    return a[k] + static_cast<unsigned>(y) * b[k] + static_cast<unsigned>(kz);
-  }
+  __device__ __forceinline__ unsigned at(int k, unsigned Y, unsigned KZ) const { return a[k] + Y * b[k] + KZ; }
   __device__ __forceinline__ bool is_self(int k) const { return (self >> k) & 1u; }
 };
+// (Y, KZ) of element (y, kz) of an exchange segment or self block (offset = segment row base +
+// Y * (rows stride) + KZ): plain [y][kx][kz] Y = y, KZ = kz; blocked (XArgs::segblk) Y = y / 8,
+// KZ = (y % 8) 8 + (kz / 8) 64 + kz % 8.  seg_stride: S of SegRows / the per-element lookups.
+__device__ __forceinline__ void seg_yk(int segblk, int y, int kz, unsigned& Y, unsigned& KZ) {
+  if (segblk) {
+    Y = static_cast<unsigned>(y) >> 3;
+    KZ = ((static_cast<unsigned>(y) & 7u) << 3) + ((static_cast<unsigned>(kz) >> 3) << 6) + (static_cast<unsigned>(kz) & 7u);
+  } else {
+    Y = static_cast<unsigned>(y);
+    KZ = static_cast<unsigned>(kz);
+  }
+}
+__host__ __device__ inline int seg_stride(const XArgs& a) { return a.segblk ? kSpecKzBlock * a.nkzs : a.nkz; }
+
 template <int NT, int C>
 inline int seg_mode(int n, const int* start, int self_seg, long long off0) {
   if (n == 1 && self_seg < 0 && off0 == 0) return kSegOne;
@@ -333,7 +348,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   static_assert(SM != kSegRows || (NT % CW == 0 && EPT <= kSegRowsMax), "row table: a thread's rows repeat per access");
   SegRows<SM == kSegRows ? EPT : 1> rt;
   if constexpr (SM == kSegRows)
-    rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, a.nkz, tid);
+    rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, seg_stride(a), tid);
   // SEG (pencil: the x-expanded output blocked by x range) with row tables: the thread's x rows
   // x = (tid + k NT) / CWO of the store passes, looked up once like the kx rows
   constexpr int CWO = C / V;  // store accesses per x row (both halves in CMB mode)
@@ -415,14 +430,19 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
                                     static_cast<unsigned>(sizeof(T2)));
           v[k][q] = a.nt ? ld_nt(r) : r;
         } else if constexpr (SM == kSegRows) {
-          v[k][q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, y, kz));
+          unsigned Y, KZ;
+          seg_yk(a.segblk, y, kz, Y, KZ);
+          v[k][q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, Y, KZ));
         } else {
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                           : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
           const T2* b = static_cast<unsigned>(sp.idx - src.self_seg) < static_cast<unsigned>(src.nself) ? sbase : base;
+          unsigned Y, KZ;
+          seg_yk(a.segblk, y, kz, Y, KZ);
+          const long long S = seg_stride(a);
           // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
           v[k][q] = *reinterpret_cast<const CV*>(
-              b + static_cast<unsigned>(sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz));
+              b + static_cast<unsigned>(sp.off + (static_cast<long long>(Y) * sp.count + (i - sp.start)) * S + KZ));
         }
       }
     }
@@ -566,7 +586,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   static_assert(SM != kSegRows || (NT % CW == 0 && KE <= kSegRowsMax), "row table: a thread's rows repeat per pass");
   SegRows<SM == kSegRows ? KE : 1> rt;
   if constexpr (SM == kSegRows)
-    rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, a.nkz, tid);
+    rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, seg_stride(a), tid);
   // SEG (pencil: the x-expanded input blocked by x range) with row tables: the thread's x rows of
   // the fetch (x = (tid + q NT) / CW, clamped), looked up once
   constexpr bool kXRows = SEG && SM == kSegRows;
@@ -673,7 +693,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           CV w;
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, y, kz)) = w;
+          unsigned Y, KZ;
+          seg_yk(a.segblk, y, kz, Y, KZ);
+          *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ)) = w;
         }
       }
       continue;
@@ -696,7 +718,9 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
                                           : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
           T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
-          *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(y) * sp.count + (i - sp.start)) * a.nkz + kz) = w;
+          unsigned Y, KZ;
+          seg_yk(a.segblk, y, kz, Y, KZ);
+          *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Y) * sp.count + (i - sp.start)) * seg_stride(a) + KZ) = w;
         }
       }
     }
@@ -793,10 +817,25 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
       smv = rows ? kSegRows : kSegFull;
     }
   } else {
-    // one field per column (tests, and the single-block paths)
-    CH_CHECK(sm == kSegOne && a.npseg == 1 && src.self_seg < 0, "xfft_backward: exchange segments need the combine mode");
-    kern = a.kzb ? xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB, false> : xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 0, false>;
-    slv = a.kzb ? SLB : 0;
+    // one field per tile (K-SPEC's six-output mode)
+    constexpr int CW1 = Cfg::C / V;
+    const int sm1 = seg_mode<Cfg::NT, CW1>(src.nsrc, src.kx_start, src.self_seg, src.off[0]);
+    constexpr int kRowsK1 = ((2 * (NN / 3) + 1) * CW1 + Cfg::NT - 1) / Cfg::NT;
+    constexpr int SMR1 = (kRowsK1 <= kSegRowsMax && Cfg::NT % CW1 == 0) ? kSegRows : kSegFull;
+    const bool rows1 = SMR1 == kSegRows && xsegrows_enabled();
+    constexpr int SMX1 = (SMR1 == kSegRows && kXRowsK <= kSegRowsMax) ? kSegRows : kSegFull;
+    if (a.kzb) {
+      kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB, false>;
+      slv = SLB;
+    } else if (a.npseg > 1) {
+      kern = rows1 ? xfft_backward_kernel<NN, T, true, WIDE, SMX1, V, 0, false> : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V, 0, false>;
+      smv = rows1 ? SMX1 : kSegFull;
+    } else if (sm1 == kSegOne) {
+      kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, 0, false>;
+    } else {
+      kern = rows1 ? xfft_backward_kernel<NN, T, false, WIDE, SMR1, V, 0, false> : xfft_backward_kernel<NN, T, false, WIDE, kSegFull, V, 0, false>;
+      smv = rows1 ? kSegRows : kSegFull;
+    }
   }
   const int cl = a.combine ? CL : Cfg::C;
   const int kc = slv == 2 ? kSpecKzBlock : cl, yp = cl / kc;

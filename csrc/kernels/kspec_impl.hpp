@@ -880,8 +880,8 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
           vo[3][r] = om[1][r];
         }
       }
-      // (STORE2: phi goes out at the end, paired with D1 omega)
-      if constexpr (!kStore2) st.store(phi, ph);
+      // (STORE2 with the combine outputs: phi goes out at the end, paired with D1 omega)
+      if (!kStore2 || a.out6) st.store(phi, ph);
       KSPEC_STAMP(6)
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
@@ -995,6 +995,59 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     // operator) omega_x = Dw - i be v = i (be phi + al D1 omega)/k2 and omega_z = i al v - Du =
     // i (be D1 omega - al phi)/k2 (convolution_kernels.cu:46-53; mean line: u = U, omega_z = -dU/dy).
     // Three field stores instead of five per substep, and the exchange of P > 1 moves five fields.
+    if (a.out6) {
+      // The six physical-stage fields themselves (u, v, w, omega_x, omega_z; omega_y is the omega
+      // state): at one rank the x-backward then reads one field per tile (two planes of a kz block,
+      // whole 128-B lines) -- 61 vs 71 us per 6-plane chunk for the combine mode's two-input tiles,
+      // while K-SPEC takes the same 4.15 ms per substep with 9 or 7 stores (profiles/r06/)
+      // wx = Dw - i be v = i (be phi + al D1 omega)/k2 - (v terms that cancel), written as in the
+      // reference's calcOmega with D(dv) = D2 v = phi + k2 v (convolution_kernels.cu:46-53)
+      auto omx = [&](int r, double& re, double& im) {
+        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+        const double br = (be * DDr + al * dvo[2][r]) * inv_k2, bi = (be * DDi + al * dvo[3][r]) * inv_k2;
+        re = -bi + be * vo[1][r];
+        im = br - be * vo[0][r];
+      };
+      auto omz = [&](int r, double& re, double& im) {  // wz = i al v - Du ; mean line: -dU/dy
+        const double DDr = ph[0][r] + k2 * vo[0][r], DDi = ph[1][r] + k2 * vo[1][r];
+        const double ar = (al * DDr - be * dvo[2][r]) * inv_k2, ai = (al * DDi - be * dvo[3][r]) * inv_k2;
+        re = -al * vo[1][r] + ai - mf * dvo[2][r];
+        im = al * vo[0][r] - ar;
+      };
+      double x[2][R], x2[2][R];
+      if constexpr (kStore2) {
+        // v and u, then w and omega_x, behind one barrier each (tiles: the extra pair, then the
+        // staging pair, whose last readers (the phi store) passed the first pair's barrier), then
+        // omega_z through the extra tile of the first pair (its readers passed the second barrier)
+#pragma unroll
+        for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
+        st.store2_into(xt0, xt1, static_cast<T2*>(a.out[1]), vo[0], vo[1], static_cast<T2*>(a.out[0]), x[0], x[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          vel_w(r, x[0][r], x[1][r]);
+          omx(r, x2[0][r], x2[1][r]);
+        }
+        st.store2_into(st.tile, st.tile2, static_cast<T2*>(a.out[2]), x[0], x[1], static_cast<T2*>(a.out[3]), x2[0], x2[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) omz(r, x[0][r], x[1][r]);
+        st.store_into(xt0, static_cast<T2*>(a.out[5]), x[0], x[1]);
+      } else {
+        st.store(static_cast<T2*>(a.out[1]), vo[0], vo[1]);  // v
+#pragma unroll
+        for (int r = 0; r < R; ++r) vel_u(r, x[0][r], x[1][r]);
+        st.store(static_cast<T2*>(a.out[0]), x[0], x[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) vel_w(r, x[0][r], x[1][r]);
+        st.store(static_cast<T2*>(a.out[2]), x[0], x[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) omx(r, x[0][r], x[1][r]);
+        st.store(static_cast<T2*>(a.out[3]), x[0], x[1]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) omz(r, x[0][r], x[1][r]);
+        st.store(static_cast<T2*>(a.out[5]), x[0], x[1]);
+      }
+      goto outputs_done;
+    }
     if constexpr (kStore2) {
       if (a.mode == 1) {
         // phi and D1 omega, then v and D1 v, behind one barrier each (tiles: the extra pair, whose
@@ -1298,7 +1351,7 @@ static void kspec_launch_t(const YTablesDev& t, const SpecArgs& a, hipStream_t s
   }
   const int sp = kspec_split_env();
   if constexpr (kspec_split_default<R, T>()) {
-    if (sp == 1) {
+    if (sp == 1 && !a.out6) {  // (the output kernel writes the combine outputs)
       auto k1 = kspec_kernel<R, T, W, kspec_slots<R, T>(), kspec_xmode<R, T>(), PAR, 0, 1>;
       const int nt1 = (a.lines + W - 1) / W;
       dim3 g1(std::min(nt1, resident_blocks(reinterpret_cast<const void*>(k1), W * 64))), b1(W * 64);

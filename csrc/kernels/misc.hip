@@ -88,10 +88,10 @@ void symmetrize_kz0(void* q, int N, int nkx, int nkzs, int Kx, int kzb, bool fp6
 // reference re-imposed the symmetry with a full backward+forward FFT round trip of both fields
 // through the global transposes (imposeSymetry.c:5-18).
 template <typename T2>
-__global__ void kz0_pack_kernel(const T2* q, T2* col, int N, int nkx_loc, int nkz_loc) {
+__global__ void kz0_pack_kernel(const T2* q, T2* col, int N, int nkx_loc, int nkz_loc, int kzb) {
   const int y = blockIdx.x;
   for (int i = threadIdx.x; i < nkx_loc; i += blockDim.x)
-    col[static_cast<size_t>(y) * nkx_loc + i] = q[(static_cast<size_t>(y) * nkx_loc + i) * nkz_loc];
+    col[static_cast<size_t>(y) * nkx_loc + i] = q[spec_index(kzb, nkx_loc, nkz_loc, y, i, 0)];
 }
 
 template <typename T2>
@@ -105,19 +105,19 @@ __global__ void kz0_sym_dist_kernel(T2* q, const T2* col, Kz0SymArgs a) {
       if (igp >= a.kx_start[r]) c = r;
     const int cnt = a.kx_start[c + 1] - a.kx_start[c];
     const T2 vp = col[static_cast<size_t>(a.N) * a.kx_start[c] + static_cast<size_t>(y) * cnt + (igp - a.kx_start[c])];
-    T2* dst = q + (static_cast<size_t>(y) * a.nkx_loc + i) * a.nkz_loc;
+    T2* dst = q + spec_index(a.kzb, a.nkx_loc, a.nkz_loc, y, i, 0);
     const T2 v = *dst;
     *dst = T2{static_cast<decltype(v.x)>(0.5 * (v.x + vp.x)), static_cast<decltype(v.x)>(0.5 * (v.y - vp.y))};
   }
 }
 
-void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, bool fp64, hipStream_t s) {
+void kz0_pack(const void* q, void* col, int N, int nkx_loc, int nkz_loc, int kzb, bool fp64, hipStream_t s) {
   if (fp64)
     hipLaunchKernelGGL(kz0_pack_kernel<double2>, dim3(N), dim3(128), 0, s, static_cast<const double2*>(q),
-                       static_cast<double2*>(col), N, nkx_loc, nkz_loc);
+                       static_cast<double2*>(col), N, nkx_loc, nkz_loc, kzb);
   else
     hipLaunchKernelGGL(kz0_pack_kernel<float2>, dim3(N), dim3(128), 0, s, static_cast<const float2*>(q),
-                       static_cast<float2*>(col), N, nkx_loc, nkz_loc);
+                       static_cast<float2*>(col), N, nkx_loc, nkz_loc, kzb);
   HIP_LAUNCH_CHECK(s);
 }
 
@@ -154,10 +154,21 @@ __global__ void __launch_bounds__(256) spectra_kernel(SpectraArgs a) {
     const size_t idx = spec_index(a.kzb, a.nkx_loc, a.nkzs, j, ikx, kl);
     const double wgt = (kx == 0 && kz == 0) ? 0.0 : (kz == 0 ? 1.0 : 2.0);
     const double be = a.az * kz, k2 = al * al + be * be, r = k2 > 0.0 ? 1.0 / k2 : 0.0;
-    const T2 d = dv[idx], o = om[idx];
-    // |u|^2 = |al D1v - be om|^2 / k2^2, |w|^2 = |be D1v + al om|^2 / k2^2 (nonLinear_kernels.cu:55-72)
-    const double ur = (al * d.x - be * o.x) * r, ui = (al * d.y - be * o.y) * r;
-    const double wr = (be * d.x + al * o.x) * r, wi = (be * d.y + al * o.y) * r;
+    double ur, ui, wr, wi;
+    if (a.combine) {
+      const T2 d = dv[idx], o = om[idx];
+      // |u|^2 = |al D1v - be om|^2 / k2^2, |w|^2 = |be D1v + al om|^2 / k2^2 (nonLinear_kernels.cu:55-72)
+      ur = (al * d.x - be * o.x) * r;
+      ui = (al * d.y - be * o.y) * r;
+      wr = (be * d.x + al * o.x) * r;
+      wi = (be * d.y + al * o.y) * r;
+    } else {
+      const T2 cu = static_cast<const T2*>(a.u)[idx], cw = static_cast<const T2*>(a.w)[idx];
+      ur = cu.x;
+      ui = cu.y;
+      wr = cw.x;
+      wi = cw.y;
+    }
     const T2 c1 = vv[idx];
     const double en[3] = {ur * ur + ui * ui, static_cast<double>(c1.x) * c1.x + static_cast<double>(c1.y) * c1.y,
                           wr * wr + wi * wi};

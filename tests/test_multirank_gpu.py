@@ -68,20 +68,25 @@ def _assemble(parts, field):
     return out
 
 
-@pytest.mark.parametrize("world,pr,chunk,self_mode", [(2, 1, "0", "direct"), (3, 1, "0", "direct"),
-                                                      (3, 1, "4", "direct"), (2, 1, "1", "direct"),
-                                                      (3, 1, "4", "copy"), (2, 2, "0", "direct"),
-                                                      (4, 2, "0", "direct"), (4, 2, "4", "direct"),
-                                                      (4, 2, "5", "copy"), (6, 2, "3", "direct"),
-                                                      (6, 3, "4", "direct")])
-def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mode):
+@pytest.mark.parametrize("world,pr,chunk,self_mode,kzb", [(2, 1, "0", "direct", "0"), (3, 1, "0", "direct", "0"),
+                                                          (3, 1, "4", "direct", "0"), (2, 1, "1", "direct", "0"),
+                                                          (3, 1, "4", "copy", "0"), (2, 2, "0", "direct", "0"),
+                                                          (4, 2, "0", "direct", "0"), (4, 2, "4", "direct", "0"),
+                                                          (4, 2, "5", "copy", "0"), (6, 2, "3", "direct", "0"),
+                                                          (6, 3, "4", "direct", "0"),
+                                                          (3, 1, "8", "direct", "1"), (2, 1, "0", "copy", "1"),
+                                                          (4, 2, "8", "direct", "1"), (6, 2, "8", "direct", "1")])
+def test_multirank_matches_oracle(native, monkeypatch, world, pr, chunk, self_mode, kzb):
     """chunk: y planes per exchange chunk of the slab and pencil pipelines (0 = whole slab; 4 with
     NY=33 over 3 ranks gives uneven ranks a different number of non-empty chunks); self_mode: own
     block in place (direct) or copied inside the exchange (copy).  pr > 1: pencil grids pr x
     world/pr, the chunked software pipeline with the row-group (B) exchange on its own group
-    communicator."""
+    communicator.  kzb = 1: the blocked spectral layout at P > 1 (CHANNEL_SPEC_KZB=1; the default at
+    R = 7, 8): y split in whole 8-plane tiles (NY = 33 over 3: 8 / 16 / 9 rows), exchange blocks
+    and segments in tiles, the distributed kz = 0 symmetrisation on blocked fields."""
     monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
     monkeypatch.setenv("CHANNEL_A2A_SELF", self_mode)
+    monkeypatch.setenv("CHANNEL_SPEC_KZB", kzb)
     nsteps = 2
     ref = ora.OracleSolver(**GRID, Re=400.0, dt_fixed=0.01)
     phi, om, U = _global_state()
@@ -182,7 +187,11 @@ def test_eight_ranks_uneven_realistic_shape(native, monkeypatch, pr):
 
     cfg = default_config(**grid, Re=2000.0, precision="fp64", ic="random", ic_amplitude=0.05, stats_every=0,
                          log_every=0, symmetry_every=0)
+    # the single-rank reference in the combine mode of P > 1 (K-SPEC's D1 v / v / D1 omega outputs,
+    # the combining x-backward), the arithmetic the 8 ranks run
+    monkeypatch.setenv("CHANNEL_COMBINE", "1")
     s1 = native.Solver(cfg, 0, 1, 0, b"")
+    assert s1.combine()
     s1.init_ic()
     s1.prepare()
     for _ in range(nsteps):

@@ -291,3 +291,42 @@ def test_rccl_two_compute_streams_captured_torch_free(native):
     env = dict(os.environ, CHANNEL_TORCH_FREE="1", CHANNEL_PSTREAMS="2", CHANNEL_YCHUNK="16", CHANNEL_ROOT=root)
     r = subprocess.run([sys.executable, "-c", PSTREAMS_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "PSTREAMS_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("kblocks,chunk,precision,combine", [("1", "8", "fp64", "0"), ("4", "16", "fp64", "0"),
+                                                             ("16", "8", "fp64", "1"), ("4", "0", "fp32", "0"),
+                                                             ("4", "16", "fp32", "1")])
+def test_rccl_blocked_layout_equals_fast_path(native, monkeypatch, kblocks, chunk, precision, combine):
+    """The blocked spectral layout ([y/8][line/8][y%8][line%8], the default at R = 7, 8) on the P > 1
+    pipeline (CHANNEL_SPEC_KZB=1 on both sides): kx sub-blocks each blocked, exchange chunks of whole
+    8-plane tiles, the x kernels addressing blocked exchange segments and self blocks (segblk).
+    State and the kz = 0 symmetrisation equal the one-rank fast path on the same layout bitwise, the
+    statistics and spectra to summation order."""
+    monkeypatch.setenv("CHANNEL_SPEC_KZB", "1")
+    monkeypatch.setenv("CHANNEL_YCHUNK", chunk)
+    monkeypatch.setenv("CHANNEL_COMBINE", combine)  # (combine = 1: the P > 1 default, on both sides)
+    res = []
+    for uid, kb in ((b"", None), (native.new_unique_id(), kblocks)):
+        if kb is not None:
+            monkeypatch.setenv("CHANNEL_KBLOCKS", kb)
+        cfg = default_config(**{**KW, "precision": precision, "stats_every": 1, "spectra_planes": "0,10,32"})
+        s = native.Solver(cfg, 0, 1, 0, uid)
+        assert s.spec_kzb() == 8
+        if kb is not None:
+            assert s.kblocks() == int(kb)
+        s.init_ic()
+        s.prepare()
+        for i in range(3):
+            s.step(True)
+        s.symmetrize()
+        s.prepare()
+        s.step(True)
+        sp = s.spectra()
+        res.append((s.get_state(), np.asarray(s.stats()), sp))
+        del s
+    (a, sa, pa), (b, sb, pb) = res
+    for f in range(3):
+        assert np.array_equal(a[f], b[f]), f"field {f}"
+    assert np.allclose(sa, sb, rtol=1e-12, atol=0)  # (atomic plane sums: summation order)
+    for k in ("ekx", "ekz", "map"):
+        assert np.allclose(pa[k], pb[k], rtol=1e-12, atol=0), k

@@ -181,8 +181,9 @@ def test_two_rank_driver_files_decode(native, tmp_path):
         conf = os.path.join(d, "run.conf")
         with open(conf, "w") as f:
             f.write(CONF.format(d=d))
-        if P == 1:
-            r = subprocess.run([BIN, conf, "--quiet"], capture_output=True, text=True, timeout=300)
+        if P == 1:  # (in the combine mode the two ranks use: the same arithmetic)
+            r = subprocess.run([BIN, conf, "--quiet"], capture_output=True, text=True, timeout=300,
+                               env=dict(os.environ, CHANNEL_COMBINE="1"))
             assert r.returncode == 0, r.stderr
         else:
             sk = socket.socket()

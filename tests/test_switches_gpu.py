@@ -23,7 +23,10 @@ rng = np.random.default_rng(7)
 Nzp = 1024
 nkz = Nzp // 3 + 1
 for dtype, tol in ((torch.complex64, 5e-6), (torch.complex128, 1e-12)):
-    for NX, ny in ((5, 3), (16, 3), (7, 1)):  # 15, 48 and 7 rows: odd row counts leave a row unpaired
+    # rows = ny * NX (a multiple of the block's 4 rows): 48 and 40 rows give every wave of the
+    # persistent grid one row (ZFFT=4: the unpaired tail path), 3072 rows more groups than the
+    # grid holds (blocks walk one or two groups: paired and unpaired waves)
+    for NX, ny in ((16, 3), (8, 5), (64, 48)):
         f = rng.standard_normal((6, ny, NX, nkz)) + 1j * rng.standard_normal((6, ny, NX, nkz))
         f[..., 0] = f[..., 0].real
         H, m = C.zphys(torch.tensor(f, dtype=dtype, device="cuda"), Nzp, torch.ones(ny, dtype=torch.float64), 1.0, 1.0)
@@ -48,8 +51,8 @@ def _child(script, env_extra, token, timeout=300):
 @pytest.mark.parametrize("mode", ["0", "1", "2", "4"])
 def test_zfft_row_plans(mode):
     """CHANNEL_ZFFT = 0 (LDS twiddles), 1 (register twiddles), 2 (16 x 16 x 4 with pad-per-32 rows),
-    4 (paired-row H_z: two rows' H_z as one transform, the odd row of a wave through hzbuf); the
-    default 3 runs in test_kernels_gpu.py::test_zphys."""
+    4 (paired-row H_z: two rows' H_z as one transform, the odd row of a wave through hzbuf, alone);
+    the default 3 runs in test_kernels_gpu.py::test_zphys."""
     _child(ZSTAGE_SCRIPT, {"CHANNEL_ZFFT": mode}, "ZSTAGE_OK")
 
 
@@ -114,8 +117,10 @@ print("SEGROWS_OK")
 """
 
 
-def test_xsegrows_off_is_bitwise():
+@pytest.mark.parametrize("combine", ["0", "1"])
+def test_xsegrows_off_is_bitwise(combine):
     """CHANNEL_XSEGROWS=0: the P > 1 x kernels (1-rank RCCL communicator, 4 kx sub-blocks = 4
     exchange segments incl. the self blocks) with per-element segment lookups instead of the
-    per-thread row tables, bitwise against the single-rank fast path."""
-    _child(SEGROWS_SCRIPT, {"CHANNEL_XSEGROWS": "0"}, "SEGROWS_OK")
+    per-thread row tables, bitwise against the single-rank fast path; with K-SPEC's six outputs
+    and in the combine mode (CHANNEL_COMBINE=1 on both sides)."""
+    _child(SEGROWS_SCRIPT, {"CHANNEL_XSEGROWS": "0", "CHANNEL_COMBINE": combine}, "SEGROWS_OK")

@@ -20,7 +20,7 @@ from channel_gpu_amd.utils.config import default_config  # noqa: E402
 
 C = require_core()  # (imports torch first unless CHANNEL_TORCH_FREE=1)
 C.install_crash_handler()
-hip = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_NOLOAD | ctypes.RTLD_GLOBAL)
+hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
 v = ctypes.c_int(0)
 hip.hipRuntimeGetVersion(ctypes.byref(v))
 maps = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln or "librccl" in ln]
