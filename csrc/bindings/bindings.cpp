@@ -286,6 +286,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("zphys", &zphys_op);
   m.def("xfft_last_variant", [] { return xfft_last_variant(); },
         "template arguments of the last x-transform launch (rocprofv3 kernel-name form)");
+  m.def("xfft_last_backward_variant", [] { return xfft_last_backward_variant(); },
+        "template arguments of the last x-backward launch (rocprofv3 kernel-name form)");
 
   // tensor views of a Solver's device buffers, attached to the _core Solver class
   py::object cls = core.attr("Solver");

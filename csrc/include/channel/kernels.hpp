@@ -209,6 +209,8 @@ void xfft_backward(const XArgs& a, const XSrc& src, void* phys, const Twiddles& 
 void xfft_forward(const XArgs& a, const void* phys, const XDst& dst, const Twiddles& tw, bool fp64, hipStream_t s);
 // template arguments of this thread's last x-transform launch, in rocprofv3's kernel-name form (tests)
 std::string xfft_last_variant();
+// the same for this thread's last x-backward launch (a solver step ends with forward transforms)
+std::string xfft_last_backward_variant();
 
 struct ZArgs {
   int NX = 0, Nzp = 0, nkz = 0, ny = 0, y0 = 0;   // NX = local x count (rows = ny * NX)

@@ -13,8 +13,11 @@ XVariant& xfft_variant_slot() {
   static thread_local XVariant v;
   return v;
 }
-std::string xfft_last_variant() {
-  const XVariant& v = xfft_variant_slot();
+static thread_local XVariant g_last_backward;
+static std::string xfft_variant_string(const XVariant& v);
+std::string xfft_last_variant() { return xfft_variant_string(xfft_variant_slot()); }
+std::string xfft_last_backward_variant() { return xfft_variant_string(g_last_backward); }
+static std::string xfft_variant_string(const XVariant& v) {
   std::string s = std::string(v.kernel) + "<" + std::to_string(v.nn) + ", " + (v.f64 ? "double" : "float") + ", " +
                   (v.seg ? "true" : "false") + ", " + std::to_string(v.wide) + ", " + std::to_string(v.sm) + ", " +
                   std::to_string(v.v) + ", " + std::to_string(v.sl);
@@ -122,6 +125,7 @@ void xfft_backward(const XArgs& a_in, const XSrc& src, void* phys, const Twiddle
   CH_CHECK(src.nsrc > 1 || src.self_seg >= 0 || static_cast<long long>(a.ny) * a.nkx * a.nkz * esz < (1LL << 32),
            "xfft_backward: a field's spectral chunk exceeds 4 GiB (use smaller y chunks)");
   CH_DISPATCH_N(a.NX, fft_xb_len<NN>(a, src, phys, tw, fp64, s));
+  g_last_backward = xfft_variant_slot();
   HIP_LAUNCH_CHECK(s);
 }
 

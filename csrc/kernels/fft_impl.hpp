@@ -150,9 +150,16 @@ struct SegRows {
   template <int NT, int CW, int NROW, int MAXS = kMaxSeg>
   __device__ __forceinline__ void build(const int* start, const long long* off, int n, int self_seg, int nself, int nkz,
                                         int tid) {
+    static_assert(NT % CW == 0, "rows tid / CW + k NT / CW");
+    build_at<NROW, MAXS>(start, off, n, self_seg, nself, nkz, tid / CW, NT / CW);
+  }
+  // rows i = r0 + k di (the plane tiles' quad lane map: r0 = quad_row(tid))
+  template <int NROW, int MAXS = kMaxSeg>
+  __device__ __forceinline__ void build_at(const int* start, const long long* off, int n, int self_seg, int nself,
+                                           int nkz, int r0, int di) {
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int i = min((tid + k * NT) / CW, NROW - 1);
+      const int i = min(r0 + k * di, NROW - 1);
       const SegPos sp = seg_find<MAXS>(start, off, n, i);
       a[k] = static_cast<unsigned>(sp.off) + static_cast<unsigned>(i - sp.start) * static_cast<unsigned>(nkz);
       b[k] = static_cast<unsigned>(sp.count) * static_cast<unsigned>(nkz);
@@ -344,11 +351,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int tid = threadIdx.x;
   const int nload = NKX * CW;
   CV v[NIN][EPT];
-  static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one source block");
+  // SL with SM = kSegRows: the P > 1 exchange segments and self blocks in the blocked layout
+  // (XArgs::segblk), read as plane tiles like the one-rank field
+  static_assert(SL == 0 || SM == kSegOne || SM == kSegRows, "blocked spectral layout: one source block or row tables");
   static_assert(SM != kSegRows || (NT % CW == 0 && EPT <= kSegRowsMax), "row table: a thread's rows repeat per access");
   SegRows<SM == kSegRows ? EPT : 1> rt;
   if constexpr (SM == kSegRows)
-    rt.template build<NT, CW, NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, seg_stride(a), tid);
+    rt.template build_at<NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, seg_stride(a),
+                              QM::on ? quad_row(tid) : tid / CW, NT / CW);
   // SEG (pencil: the x-expanded output blocked by x range) with row tables: the thread's x rows
   // x = (tid + k NT) / CWO of the store passes, looked up once like the kx rows
   constexpr int CWO = C / V;  // store accesses per x row (both halves in CMB mode)
@@ -393,6 +403,18 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
         static_assert(NT % CW == 0, "a thread's column must be the same for every access");
         constexpr int DI = NT / CW;
         const int c = (QM::on ? quad_col(tid) : tid % CW) * V, r0 = QM::on ? quad_row(tid) : tid / CW;
+        if constexpr (SM == kSegRows) {
+          // rows r0 + q DI from the row table (exchange segment or own block per row)
+          const T2* sbase = in_self(f, k);
+          unsigned Y, KZ;
+          seg_yk(1, min(y + c / KC, a.ny - 1), min(kz0 + c % KC, a.nkz - V), Y, KZ);
+#pragma unroll
+          for (int q = 0; q < EPT; ++q) {
+            const CV& r = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, Y, KZ));
+            v[k][q] = a.nt ? ld_nt(r) : r;
+          }
+          continue;
+        }
         const unsigned bt = spec_blk_off(a, min(y + c / KC, a.ny - 1), 0, min(kz0 + c % KC, a.nkz - V)) *
                             static_cast<unsigned>(sizeof(T2));
         const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
@@ -447,12 +469,58 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       }
     }
   };
+  // Deferred stores: a tile's output is read from LDS into registers (w) right after its FFT and
+  // written out after the NEXT tile is staged, ahead of that tile's prefetch.  Written straight
+  // from LDS at the end of the tile (round 5), the stores were issued after the prefetch loads, so
+  // the staging of the next tile -- whose vmcnt wait retires the memory operations in order --
+  // also waited for every store of the tile to be acknowledged, with the whole CU idle (one
+  // workgroup per CU at 147 KB of LDS); the store loop was also rolled, one LDS round trip per
+  // store.  Now the stores have a whole FFT to drain before the next wait.
+  constexpr int KS = (NX * CWO + NT - 1) / NT;  // store accesses per thread and tile
+  static_assert(NT % CWO == 0, "a thread's store column is the same for every access");
+  CV w[KS];
+  auto read_out = [&]() {
+    const int c = (tid % CWO) * V;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int x = min(tid / CWO + k * (NT / CWO), NX - 1);
+#pragma unroll
+      for (int u = 0; u < V; ++u) w[k].c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+    }
+  };
+  auto store_out = [&](int tt) {
+    int f, y, kz0;
+    decode(tt, f, y, kz0);
+    // output field of LDS column c (CMB: the group's two outputs) and its kz / plane
+    const int c = (tid % CWO) * V;
+    const int cc = c % CL;
+    const int kz = kz0 + cc % KC, yy = y + cc / KC;
+    if (kz >= a.nkz || yy >= a.ny) return;
+    const int fo = CMB ? (c < CL ? cmb_out_a(f) : cmb_out_b(f)) : f;
+    T2* out = phys + fo * a.field_stride_phys;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int x = tid / CWO + k * (NT / CWO);
+      if (KS * NT == NX * CWO || x < NX) {
+        if constexpr (kXRows) {
+          *reinterpret_cast<CV*>(out + xt.at(k, yy, kz)) = w[k];
+        } else if constexpr (SEG) {
+          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w[k];
+        } else {
+          at_byte(reinterpret_cast<CV*>(out), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
+                                               static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w[k];
+        }
+      }
+    }
+  };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
+  int tp = -1;  // tile whose output w holds
   for (; t < ntiles; t += G) {
     int f, y, kz0;
     decode(t, f, y, kz0);
-    lds_barrier();  // previous tile's stores have finished reading s
+    lds_barrier();  // the previous tile's output has been read from s
     // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
     // state, whose mean line holds U(y)); it is kx row i = 0, the kz-0 column of each plane
     const bool zmean = !CMB && f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
@@ -499,6 +567,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
+    if (tp >= 0) store_out(tp);
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
@@ -512,45 +581,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           wave_fft<NX, RB, PITCH, true, TPR, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
-    // output field of LDS column c (CMB: the group's two outputs) and its kz / plane
-    const int fa = CMB ? cmb_out_a(f) : f, fb = CMB ? cmb_out_b(f) : f;
-    T2* outa = phys + fa * a.field_stride_phys;
-    T2* outb = phys + fb * a.field_stride_phys;
-    if constexpr (kXRows) {
-#pragma unroll
-      for (int k = 0; k < KXS; ++k) {
-        const int e = tid + k * NT;
-        const int x = e / CWO, c = (e - x * CWO) * V;
-        const int cc = c % CL;
-        const int kz = kz0 + cc % KC, yy = y + cc / KC;
-        if (e < NX * CWO && kz < a.nkz && yy < a.ny) {
-          CV w;
-#pragma unroll
-          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          *reinterpret_cast<CV*>((c < CL ? outa : outb) + xt.at(k, yy, kz)) = w;
-        }
-      }
-      continue;
-    }
-    for (int e = tid; e < NX * CWO; e += NT) {
-      const int x = e / CWO, c = (e - x * CWO) * V;
-      const int cc = c % CL;
-      const int kz = kz0 + cc % KC, yy = y + cc / KC;
-      if (kz < a.nkz && yy < a.ny) {
-        CV w;
-#pragma unroll
-        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-        T2* out = c < CL ? outa : outb;
-        if constexpr (SEG) {
-          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
-          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
-        } else {
-          at_byte(reinterpret_cast<CV*>(out), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
-                                               static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
-        }
-      }
-    }
+    read_out();
+    tp = t;
   }
+  if (tp >= 0) store_out(tp);
 }
 
 template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
@@ -581,7 +615,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   const int G = static_cast<int>(gridDim.x);
   const int tid = threadIdx.x;
   CV v[EPT];
-  static_assert(SL == 0 || SM == kSegOne, "blocked spectral layout: one destination block");
+  static_assert(SL == 0 || SM == kSegOne || SM == kSegRows, "blocked spectral layout: one destination block or row tables");
   constexpr int KE = (NKX * CW + NT - 1) / NT;  // store passes over the retained kx rows
   static_assert(SM != kSegRows || (NT % CW == 0 && KE <= kSegRowsMax), "row table: a thread's rows repeat per pass");
   SegRows<SM == kSegRows ? KE : 1> rt;
@@ -629,12 +663,69 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       }
     }
   };
+  // deferred stores (as in xfft_backward_kernel): the retained kx rows of a tile go from LDS into
+  // registers after its FFT and out after the next tile is staged, ahead of its prefetch
+  static_assert(NT % CW == 0, "a thread's store column is the same for every access");
+  constexpr int DI = NT / CW;  // kx rows between a thread's store accesses
+  CV w[KE];
+  auto read_out = [&]() {
+    const int c = (tid % CW) * V;
+#pragma unroll
+    for (int k = 0; k < KE; ++k) {
+      const int i = min(tid / CW + k * DI, NKX - 1);
+      const int x = i <= KXH ? i : NX - (NKX - i);
+#pragma unroll
+      for (int u = 0; u < V; ++u) w[k].c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+    }
+  };
+  auto store_out = [&](int tt) {
+    int f, y, kz0;
+    decode(tt, f, y, kz0);
+    const int c = (tid % CW) * V;
+    const int kz = kz0 + c % KC, yy = y + c / KC;
+    if (kz >= a.nkz || yy >= a.ny) return;
+    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    // this rank's own block goes straight into its spectral field (no self exchange)
+    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
+    unsigned Y = 0, KZ = 0;
+    if constexpr (SM == kSegRows) seg_yk(a.segblk, yy, kz, Y, KZ);
+    unsigned ot = 0;
+    if constexpr (SL && SM != kSegRows) ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
+    const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
+#pragma unroll
+    for (int k = 0; k < KE; ++k) {
+      const int i = tid / CW + k * DI;
+      if (!(KE * NT == NKX * CW || i < NKX)) continue;
+      if constexpr (SM == kSegRows) {
+        CV& r = *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ));
+        if (SL && a.nt) st_nt(r, w[k]);
+        else r = w[k];
+      } else if constexpr (SL) {
+        CV& r = at_byte(reinterpret_cast<CV*>(outb), ot + static_cast<unsigned>(i) * rs);
+        if (a.nt) st_nt(r, w[k]);
+        else r = w[k];
+      } else if constexpr (SM == kSegOne) {
+        CV& r = at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(yy * NKX + i) * static_cast<unsigned>(a.nkz) +
+                                                      static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
+        if (a.nt) st_nt(r, w[k]);
+        else r = w[k];
+      } else {
+        const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, k * DI, DI, i)
+                                        : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
+        T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
+        unsigned Ys, KZs;
+        seg_yk(a.segblk, yy, kz, Ys, KZs);
+        *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Ys) * sp.count + (i - sp.start)) * seg_stride(a) + KZs) = w[k];
+      }
+    }
+  };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
+  int tp = -1;  // tile whose output w holds
   for (; t < ntiles; t += G) {
     int f, y, kz0;
     decode(t, f, y, kz0);
-    lds_barrier();
+    lds_barrier();  // the previous tile's output has been read from s
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -646,6 +737,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
+    if (tp >= 0) store_out(tp);
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
@@ -659,72 +751,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           wave_fft<NX, RB, PITCH, false, TPR, false, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
-    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
-    if constexpr (SL) {
-      // one column per thread (NT % CW == 0), kx rows one block-column stride apart
-      static_assert(NT % CW == 0, "a thread's column must be the same for every access");
-      const int c = (tid % CW) * V;
-      const int kz = kz0 + c % KC, yy = y + c / KC;
-      if (kz < a.nkz && yy < a.ny) {
-        const unsigned ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
-        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
-        CV* ov = reinterpret_cast<CV*>(outb);
-        for (int i = tid / CW; i < NKX; i += NT / CW) {
-          const int x = i <= KXH ? i : NX - (NKX - i);
-          CV w;
-#pragma unroll
-          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          if (a.nt) st_nt(at_byte(ov, ot + static_cast<unsigned>(i) * rs), w);
-          else at_byte(ov, ot + static_cast<unsigned>(i) * rs) = w;
-        }
-      }
-      continue;
-    }
-    // this rank's own block goes straight into its spectral field (no self exchange)
-    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
-    if constexpr (SM == kSegRows) {
-#pragma unroll
-      for (int k = 0; k < KE; ++k) {
-        const int e = k * NT + tid;
-        const int i = e / CW, c = (e - i * CW) * V;
-        const int kz = kz0 + c % KC, yy = y + c / KC;
-        if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
-          const int x = i <= KXH ? i : NX - (NKX - i);
-          CV w;
-#pragma unroll
-          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-          unsigned Y, KZ;
-          seg_yk(a.segblk, y, kz, Y, KZ);
-          *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ)) = w;
-        }
-      }
-      continue;
-    }
-    for (int e0 = 0; e0 < NKX * CW; e0 += NT) {
-      const int e = e0 + tid;
-      const int i = e / CW, c = (e - i * CW) * V;
-      const int kz = kz0 + c % KC, yy = y + c / KC;
-      if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
-        const int x = i <= KXH ? i : NX - (NKX - i);
-        CV w;
-#pragma unroll
-        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-        if constexpr (SM == kSegOne) {
-          CV& r = at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) +
-                                                        static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
-          if (a.nt) st_nt(r, w);
-          else r = w;
-        } else {
-          const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
-                                          : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
-          T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
-          unsigned Y, KZ;
-          seg_yk(a.segblk, y, kz, Y, KZ);
-          *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Y) * sp.count + (i - sp.start)) * seg_stride(a) + KZ) = w;
-        }
-      }
-    }
+    read_out();
+    tp = t;
   }
+  if (tp >= 0) store_out(tp);
 }
 
 // The template arguments of the last x-transform launch of this thread, as in the rocprofv3 kernel
@@ -807,6 +837,11 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
     if (a.kzb) {
       kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLC, true>;
       slv = SLC;
+    } else if (a.segblk && a.npseg == 1 && rows && SMR == kSegRows) {
+      // P > 1, blocked exchange segments: plane tiles through the row table
+      kern = xfft_backward_kernel<NN, T, false, WIDE, (SMR == kSegRows ? kSegRows : kSegOne), V, (SMR == kSegRows ? SLC : 0), true>;
+      smv = kSegRows;
+      slv = SLC;
     } else if (a.npseg > 1) {
       kern = rows ? xfft_backward_kernel<NN, T, true, WIDE, SMX, V, 0, true> : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V, 0, true>;
       smv = rows ? SMX : kSegFull;
@@ -827,6 +862,10 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
     if (a.kzb) {
       kern = xfft_backward_kernel<NN, T, false, WIDE, kSegOne, V, SLB, false>;
       slv = SLB;
+    } else if (a.segblk && a.npseg == 1 && rows1 && SMR1 == kSegRows) {
+      kern = xfft_backward_kernel<NN, T, false, WIDE, (SMR1 == kSegRows ? kSegRows : kSegOne), V, (SMR1 == kSegRows ? SLB : 0), false>;
+      smv = kSegRows;
+      slv = SLB;
     } else if (a.npseg > 1) {
       kern = rows1 ? xfft_backward_kernel<NN, T, true, WIDE, SMX1, V, 0, false> : xfft_backward_kernel<NN, T, true, WIDE, kSegFull, V, 0, false>;
       smv = rows1 ? SMX1 : kSegFull;
@@ -840,7 +879,7 @@ static void xb_launch_cfg(const XArgs& a, const XSrc& src, void* phys, const Twi
   const int cl = a.combine ? CL : Cfg::C;
   const int kc = slv == 2 ? kSpecKzBlock : cl, yp = cl / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * (a.combine ? kCmbGroups : a.nfields);
-  xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, !a.kzb && a.npseg > 1, WIDE, smv, V, slv, a.combine ? 1 : 0);
+  xfft_note_variant("xfft_backward_kernel", NN, sizeof(T) == 8, !a.kzb && !slv && a.npseg > 1, WIDE, smv, V, slv, a.combine ? 1 : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XB_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, src, static_cast<T2*>(phys), static_cast<const T2*>(tw.buf));
 }
@@ -861,17 +900,20 @@ static void xf_launch_cfg(const XArgs& a, const void* phys, const XDst& dst, con
   const bool rows = SMR == kSegRows && xsegrows_enabled();
   constexpr int kXRowsK = (NN * (Cfg::C / V) + Cfg::NT - 1) / Cfg::NT;
   constexpr int SMX = (SMR == kSegRows && kXRowsK <= kSegRowsMax) ? kSegRows : kSegFull;
+  const bool segsl = !a.kzb && a.segblk && a.npseg == 1 && rows && SMR == kSegRows;  // P > 1 plane tiles
   auto kern = a.kzb                   ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V, SLB>
+              : segsl                 ? xfft_forward_kernel<NN, T, false, WIDE, (SMR == kSegRows ? kSegRows : kSegOne), V, (SMR == kSegRows ? SLB : 0)>
               : a.npseg > 1           ? (rows ? xfft_forward_kernel<NN, T, true, WIDE, SMX, V>
                                               : xfft_forward_kernel<NN, T, true, WIDE, kSegFull, V>)
               : sm == kSegOne ? xfft_forward_kernel<NN, T, false, WIDE, kSegOne, V>
               : rows          ? xfft_forward_kernel<NN, T, false, WIDE, SMR, V>
               : sm == kSegWin ? xfft_forward_kernel<NN, T, false, WIDE, kSegWin, V>
                               : xfft_forward_kernel<NN, T, false, WIDE, kSegFull, V>;
-  const int kc = (a.kzb && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
+  const int kc = ((a.kzb || segsl) && SLB == 2) ? kSpecKzBlock : Cfg::C, yp = Cfg::C / kc;
   const int ntiles = (a.ny + yp - 1) / yp * ((a.nkz + kc - 1) / kc) * a.nfields;
-  xfft_note_variant("xfft_forward_kernel", NN, sizeof(T) == 8, a.kzb ? 0 : (a.npseg > 1), WIDE,
-                    a.kzb ? kSegOne : (a.npseg > 1 ? (rows ? SMX : kSegFull) : (sm != kSegOne && rows ? kSegRows : sm)), V, a.kzb ? SLB : 0);
+  xfft_note_variant("xfft_forward_kernel", NN, sizeof(T) == 8, (a.kzb || segsl) ? 0 : (a.npseg > 1), WIDE,
+                    a.kzb ? kSegOne : segsl ? kSegRows : (a.npseg > 1 ? (rows ? SMX : kSegFull) : (sm != kSegOne && rows ? kSegRows : sm)), V,
+                    (a.kzb || segsl) ? SLB : 0);
   dim3 grid(std::min(ntiles, persist_blocks(reinterpret_cast<const void*>(kern), Cfg::NT, "CHANNEL_XF_BPC")));
   hipLaunchKernelGGL(kern, grid, dim3(Cfg::NT), 0, s, a, static_cast<const T2*>(phys), dst,
                      static_cast<const T2*>(tw.buf));
@@ -1817,7 +1859,7 @@ void fft_xb_len(const XArgs& a, const XSrc& src, void* phys, const Twiddles& tw,
   if (fp64) {
     xb_launch_cfg<NN, double, 0>(a, src, phys, tw, s);
   } else if constexpr (NN == 512 || NN == 1024) {
-    if (xwide_enabled() || (a.kzb && xplanes_enabled())) xb_launch_cfg<NN, float, 1>(a, src, phys, tw, s);
+    if (xwide_enabled() || ((a.kzb || a.segblk) && xplanes_enabled())) xb_launch_cfg<NN, float, 1>(a, src, phys, tw, s);
     else xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
   } else {
     xb_launch_cfg<NN, float, 0>(a, src, phys, tw, s);
@@ -1828,7 +1870,7 @@ void fft_xf_len(const XArgs& a, const void* phys, const XDst& dst, const Twiddle
   if (fp64) {
     xf_launch_cfg<NN, double, 0>(a, phys, dst, tw, s);
   } else if constexpr (NN == 512 || NN == 1024) {
-    if (xwide_enabled() || (a.kzb && xplanes_enabled())) xf_launch_cfg<NN, float, 1>(a, phys, dst, tw, s);
+    if (xwide_enabled() || ((a.kzb || a.segblk) && xplanes_enabled())) xf_launch_cfg<NN, float, 1>(a, phys, dst, tw, s);
     else xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);
   } else {
     xf_launch_cfg<NN, float, 0>(a, phys, dst, tw, s);

@@ -330,3 +330,35 @@ def test_rccl_blocked_layout_equals_fast_path(native, monkeypatch, kblocks, chun
     assert np.allclose(sa, sb, rtol=1e-12, atol=0)  # (atomic plane sums: summation order)
     for k in ("ekx", "ekz", "map"):
         assert np.allclose(pa[k], pb[k], rtol=1e-12, atol=0), k
+
+
+@pytest.mark.parametrize("combine", ["0", "1"])
+def test_rccl_blocked_plane_tiles_equal_fast_path(native, monkeypatch, combine):
+    """The x kernels of the P > 1 pipeline on the blocked layout as plane tiles (two planes x one
+    8-wide kz block per 128-B line, the one-rank fast path's tiles; WIDE = 1 at NX = 512 / 1024 fp32)
+    with each row's exchange segment or own block from the per-thread row table: bitwise the
+    one-rank fast path, and the launched variants are the plane-tile row-table ones."""
+    monkeypatch.setenv("CHANNEL_SPEC_KZB", "1")
+    monkeypatch.setenv("CHANNEL_YCHUNK", "8")
+    monkeypatch.setenv("CHANNEL_COMBINE", combine)
+    res = []
+    for uid, kb in ((b"", None), (native.new_unique_id(), "4")):
+        if kb is not None:
+            monkeypatch.setenv("CHANNEL_KBLOCKS", kb)
+        cfg = default_config(**{**KW, "NX": 512, "NY": 65, "NZ": 129, "precision": "fp32", "Re": 2000.0})
+        s = native.Solver(cfg, 0, 1, 0, uid)
+        assert s.spec_kzb() == 8
+        s.init_ic()
+        s.prepare()
+        for _ in range(3):
+            s.step(False)
+        res.append(s.get_state())
+        if kb is not None:
+            assert s.comm_kind() == "rccl"
+            assert native.xfft_last_variant() == "xfft_forward_kernel<512, float, false, 1, 3, 2, 2>", native.xfft_last_variant()
+            bw = native.xfft_last_backward_variant()
+            assert bw == f"xfft_backward_kernel<512, float, false, 1, 3, 2, 2, {'true' if combine == '1' else 'false'}>", bw
+        del s
+    a, b = res
+    for f in range(3):
+        assert np.array_equal(a[f], b[f]), f"field {f}"

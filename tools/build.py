@@ -107,6 +107,9 @@ def build(verbose: bool = False, jobs: int = 8, driver: bool = True) -> None:
     hdr = _newest_header()
     srcs = sorted(glob.glob(os.path.join(ROOT, "csrc", "core", "*.cpp")) +
                   glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.hip")))
+    # longest compiles first (the 1024/2048-point transform units and K-SPEC take minutes each)
+    heavy = ("fft_pow2_1024", "fft_pow2_2048", "kspec", "fft_pow2.", "fft_r")
+    srcs.sort(key=lambda s: next((i for i, h in enumerate(heavy) if h in os.path.basename(s)), len(heavy)))
     objs, jobs_list = [], []
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")

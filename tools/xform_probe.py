@@ -4,6 +4,7 @@ the pipeline switches (CHANNEL_YCHUNK, CHANNEL_YSTREAMS, CHANNEL_FFT_DIAG, ...),
 per process: run one process per setting.
 
   python tools/xform_probe.py --grid 1024x385x1024 --reps 20      -> one JSON line
+  --force-comm: the P > 1 pipeline on a 1-rank RCCL communicator (exchange segments, kx sub-blocks)
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ def main() -> None:
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--force-comm", action="store_true")
     args = ap.parse_args()
     os.environ["CHANNEL_TORCH_FREE"] = "1"
     from channel_gpu_amd import require_core
@@ -32,7 +34,7 @@ def main() -> None:
     NX, NY, NZP = (int(v) for v in args.grid.lower().split("x"))
     cfg = default_config(NX=NX, NY=NY, NZ=NZP // 2 + 1, Re=20700.0, precision=args.precision, ic="random",
                          ic_amplitude=0.05, stats_every=0, log_every=0, symmetry_every=0)
-    s = C.Solver(cfg, 0, 1, 0, b"")
+    s = C.Solver(cfg, 0, 1, 0, C.new_unique_id() if args.force_comm else b"")
     s.init_ic()
     s.prepare()
     for _ in range(args.warmup):
@@ -45,7 +47,7 @@ def main() -> None:
     ms = 1e3 * (time.perf_counter() - t0) / args.reps
     env = {k: v for k, v in os.environ.items() if k.startswith("CHANNEL_") and k != "CHANNEL_TORCH_FREE"}
     print(json.dumps({"grid": args.grid, "precision": args.precision, "ms_per_substep_transforms": round(ms, 4),
-                      "ms_per_step_transforms": round(3 * ms, 3), "env": env}), flush=True)
+                      "ms_per_step_transforms": round(3 * ms, 3), "comm": s.comm_kind(), "env": env}), flush=True)
 
 
 if __name__ == "__main__":
