@@ -354,7 +354,39 @@ void Solver::alloc() {
   HIP_CHECK(hipEventCreateWithFlags(&ev_fwd_done_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_red_, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&ev_stats_, hipEventDisableTiming));
+  for (auto& e : ev_dtf_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   ph_ms_.assign(8, 0.0);
+  if (comm_ && !p.pencil()) build_rowtab();
+}
+
+// Row table of the slab exchange segments (XSrc / XDst::rowtab): for retained kx row i of segment
+// s = c * nkb_ + b (rank c's kx sub-block b), the element offset of row i at the first chunk (y0 = 0)
+// and the segment's Y stride (rows of 8 planes in the blocked layout, planes in the plain one), with
+// the self-block bit for this rank's own blocks (read / written in place in the spectral fields).
+// A chunk at y0 adds (y0 / 8 or y0) Y strides (XArgs::seg_y0): the offsets of transforms_slab's
+// per-chunk segment tables, without a lookup per launch.
+void Solver::build_rowtab() {
+  const Plan& p = plan_;
+  const int NB = nkb_;
+  const long long ny_pad = spec_rows(kzb_, p.ny_loc);
+  const long long S = kzb_ ? static_cast<long long>(kSpecKzBlock) * nkzs_ : nkzs_;  // seg_stride
+  std::vector<unsigned> h(2 * static_cast<size_t>(p.nkx));
+  for (int c = 0; c < p.Pc; ++c)
+    for (int b = 0; b < NB; ++b) {
+      const bool self = self_direct_ && c == p.pcol;
+      const long long start = kb_gstart(c, b), count = kb_gcount(c, b);
+      const long long off0 = self ? static_cast<long long>(kb_off_[b]) + static_cast<long long>(p.y0) * kb_cnt_[b] * nkzs_
+                                  : ny_pad * start * nkzs_;
+      for (long long i = start; i < start + count; ++i) {
+        const long long a = off0 + (i - start) * S, st = count * S;
+        CH_CHECK(a + (ny_pad / (kzb_ ? kSpecKzBlock : 1)) * st < (1ll << 32) && st < (1ll << 31),
+                 "exchange segment offsets exceed 32 bits");
+        h[2 * i] = static_cast<unsigned>(a);
+        h[2 * i + 1] = static_cast<unsigned>(st) | (self ? 0x80000000u : 0u);
+      }
+    }
+  HIP_CHECK(hipMalloc(&d_rowtab_, h.size() * sizeof(unsigned)));
+  HIP_CHECK(hipMemcpy(d_rowtab_, h.data(), h.size() * sizeof(unsigned), hipMemcpyHostToDevice));
 }
 
 void Solver::free_all() {
@@ -387,13 +419,15 @@ void Solver::free_all() {
   ev_cb_.clear();
   ev_cc_.clear();
   step_ev_.clear();
-  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_cfl_, ev_stats_, ev_tdt_[0], ev_tdt_[1]})
+  for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_cfl_, ev_stats_, ev_tdt_[0], ev_tdt_[1], ev_dtf_[0], ev_dtf_[1]})
     if (e) (void)hipEventDestroy(e);
   if (h_tdt_) (void)hipHostFree(h_tdt_);
   h_tdt_ = nullptr;
-  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_, static_cast<void*>(d_y_)})
+  for (void* p : {state_, out_, phys_, xbuf_, zbuf_, dscal_, snap_, d_spec_, d_sym_, static_cast<void*>(d_y_),
+                  static_cast<void*>(d_rowtab_)})
     if (p) (void)hipFree(p);
   state_ = out_ = phys_ = xbuf_ = zbuf_ = dscal_ = snap_ = d_spec_ = d_sym_ = nullptr;
+  d_rowtab_ = nullptr;
   d_y_ = nullptr;
 }
 
@@ -921,11 +955,23 @@ void Solver::transforms(int n, bool /*stats*/) {
     ev(2, false);
     zphys(za, phys_, tw_z_, fp64_, s_comp_);
     ev(2, true);
-    if (n == 0) dt_update(da, s_comp_);
+    // dt from the CFL maxima on the (idle at P = 1) comm stream, beside the x-forward: only the next
+    // K-SPEC needs it (one ~5 us kernel less on the critical path of a small grid's step; phase
+    // timing keeps it in line)
+    const bool fork_dt = n == 0 && !phase_timing_;
+    if (fork_dt) {
+      HIP_CHECK(hipEventRecord(ev_dtf_[0], s_comp_));
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_dtf_[0], 0));
+      dt_update(da, s_comm_);
+      HIP_CHECK(hipEventRecord(ev_dtf_[1], s_comm_));
+    } else if (n == 0) {
+      dt_update(da, s_comp_);
+    }
     xa.nfields = 3;
     ev(3, false);
     xfft_forward(xa, phys_, dst, tw_x_, fp64_, s_comp_);
     ev(3, true);
+    if (fork_dt) HIP_CHECK(hipStreamWaitEvent(s_comp_, ev_dtf_[1], 0));
     return;
   }
   if (!p.pencil()) {
@@ -1145,6 +1191,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   for (int c = 0; c < P; ++c)
     for (int b = 0; b < NB; ++b) src.kx_start[c * NB + b] = dst.kx_start[c * NB + b] = kb_gstart(c, b);
   src.kx_start[NS] = dst.kx_start[NS] = p.nkx;
+  src.rowtab = dst.rowtab = d_rowtab_;  // (the same rows as the per-chunk off[] below, at y0 = 0)
   if (self_direct_) {  // own kx blocks: straight from / into the spectral fields
     src.self_seg = dst.self_seg = p.rank * NB;
     src.nself = dst.nself = NB;
@@ -1224,6 +1271,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
       XArgs xc = xa;
       xc.ny = ny;
       xc.nfields = 6;
+      xc.seg_y0 = kzb_ ? y0 / kSpecYBlock : y0;
       char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz_loc * esz_;
       ev(1, false, cs);
       xfft_backward(xc, src, ph, tw_x_, fp64_, cs);

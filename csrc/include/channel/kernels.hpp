@@ -159,6 +159,11 @@ struct XSrc {
   int nself = 1;
   const void* self_base = nullptr;
   long long self_field_stride = 0;
+  // per-row table of the exchange segments (row-table modes, optional): for each retained kx row i,
+  // rowtab[2 i] = element offset of row i at segment row Y = 0 of the FIRST chunk (y0 = 0),
+  // rowtab[2 i + 1] = its segment's Y stride | 0x80000000 for a self block.  Chunk rows then add
+  // XArgs::seg_y0 to Y.  Built once per run on the host (Solver::build_rowtab) instead of per launch.
+  const unsigned* rowtab = nullptr;
 };
 struct XDst {             // destination blocks for the forward x-transform (per destination rank)
   void* base = nullptr;
@@ -169,6 +174,7 @@ struct XDst {             // destination blocks for the forward x-transform (per
   int nself = 1;
   void* self_base = nullptr;
   long long self_field_stride = 0;
+  const unsigned* rowtab = nullptr;  // as XSrc::rowtab
 };
 
 struct XArgs {
@@ -195,6 +201,7 @@ struct XArgs {
   // kzb = 8 within each segment: [y/8][line/8][y%8][line%8], line = kx in segment * nkzs + kz;
   // chunk rows start on 8-plane tiles).  fft_impl.hpp seg_yk / seg_stride
   int segblk = 0;
+  int seg_y0 = 0;                    // with XSrc / XDst::rowtab: the chunk's first segment row Y
   int nt = 0;                        // streaming (non-temporal) spectral accesses (solver default 1;
                                      // CHANNEL_XNT=0 off: 35.0 vs 34.75 ms/step, profiles/r04/ab_xnt.txt)
   // backward only: combine mode -- the six output fields u, v, w, omega_x, omega_y, omega_z are

@@ -212,6 +212,9 @@ class Solver {
   void* out_ = nullptr;    // 6 * spec
   void* phys_ = nullptr;   // 6 * phys
   void* xbuf_ = nullptr;   // P>1: 6 * ny_loc*nkx*nkz_loc (A-exchange blocks)
+  hipEvent_t ev_dtf_[2] = {nullptr, nullptr};  // P = 1 one-chunk path: dt update forked beside the x-forward
+  unsigned* d_rowtab_ = nullptr;  // slab P > 1: per retained kx row, its exchange segment's offset / stride (XSrc::rowtab)
+  void build_rowtab();
   void* zbuf_ = nullptr;   // pencil: 6 * ny_loc*nx_loc*nkz (B-exchange blocks, z stage in place)
   size_t spec_ = 0, physn_ = 0, xstride_ = 0, zstride_ = 0;
   // spectral layout (spec_index): kzb_ = 8 (one rank) blocks the lines by 8 kz, with the kz line

@@ -166,6 +166,20 @@ struct SegRows {
       if (static_cast<unsigned>(sp.idx - self_seg) < static_cast<unsigned>(nself)) self |= 1u << k;
     }
   }
+  // rows i = r0 + k di from a host-built row table (XSrc::rowtab): two loads per row instead of
+  // a segment lookup per row (whose unrolled compare / select chains over kMaxSeg segments cost
+  // ~500 VALU instructions per wave and launch, against ~4 tiles per wave per launch)
+  template <int NROW>
+  __device__ __forceinline__ void load_at(const unsigned* tab, int y0, int r0, int di) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = min(r0 + k * di, NROW - 1);
+      const uint2 e = *reinterpret_cast<const uint2*>(tab + 2 * i);
+      b[k] = e.y & 0x7fffffffu;
+      a[k] = e.x + static_cast<unsigned>(y0) * b[k];
+      if (e.y >> 31) self |= 1u << k;
+    }
+  }
   __device__ __forceinline__ unsigned at(int k, unsigned Y, unsigned KZ) const { return a[k] + Y * b[k] + KZ; }
   __device__ __forceinline__ bool is_self(int k) const { return (self >> k) & 1u; }
 };
@@ -356,9 +370,13 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   static_assert(SL == 0 || SM == kSegOne || SM == kSegRows, "blocked spectral layout: one source block or row tables");
   static_assert(SM != kSegRows || (NT % CW == 0 && EPT <= kSegRowsMax), "row table: a thread's rows repeat per access");
   SegRows<SM == kSegRows ? EPT : 1> rt;
-  if constexpr (SM == kSegRows)
-    rt.template build_at<NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, seg_stride(a),
-                              QM::on ? quad_row(tid) : tid / CW, NT / CW);
+  if constexpr (SM == kSegRows) {
+    if (src.rowtab)
+      rt.template load_at<NKX>(src.rowtab, a.seg_y0, QM::on ? quad_row(tid) : tid / CW, NT / CW);
+    else
+      rt.template build_at<NKX>(src.kx_start, src.off, src.nsrc, src.self_seg, src.nself, seg_stride(a),
+                                QM::on ? quad_row(tid) : tid / CW, NT / CW);
+  }
   // SEG (pencil: the x-expanded output blocked by x range) with row tables: the thread's x rows
   // x = (tid + k NT) / CWO of the store passes, looked up once like the kx rows
   constexpr int CWO = C / V;  // store accesses per x row (both halves in CMB mode)
@@ -469,58 +487,12 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       }
     }
   };
-  // Deferred stores: a tile's output is read from LDS into registers (w) right after its FFT and
-  // written out after the NEXT tile is staged, ahead of that tile's prefetch.  Written straight
-  // from LDS at the end of the tile (round 5), the stores were issued after the prefetch loads, so
-  // the staging of the next tile -- whose vmcnt wait retires the memory operations in order --
-  // also waited for every store of the tile to be acknowledged, with the whole CU idle (one
-  // workgroup per CU at 147 KB of LDS); the store loop was also rolled, one LDS round trip per
-  // store.  Now the stores have a whole FFT to drain before the next wait.
-  constexpr int KS = (NX * CWO + NT - 1) / NT;  // store accesses per thread and tile
-  static_assert(NT % CWO == 0, "a thread's store column is the same for every access");
-  CV w[KS];
-  auto read_out = [&]() {
-    const int c = (tid % CWO) * V;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      const int x = min(tid / CWO + k * (NT / CWO), NX - 1);
-#pragma unroll
-      for (int u = 0; u < V; ++u) w[k].c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-    }
-  };
-  auto store_out = [&](int tt) {
-    int f, y, kz0;
-    decode(tt, f, y, kz0);
-    // output field of LDS column c (CMB: the group's two outputs) and its kz / plane
-    const int c = (tid % CWO) * V;
-    const int cc = c % CL;
-    const int kz = kz0 + cc % KC, yy = y + cc / KC;
-    if (kz >= a.nkz || yy >= a.ny) return;
-    const int fo = CMB ? (c < CL ? cmb_out_a(f) : cmb_out_b(f)) : f;
-    T2* out = phys + fo * a.field_stride_phys;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      const int x = tid / CWO + k * (NT / CWO);
-      if (KS * NT == NX * CWO || x < NX) {
-        if constexpr (kXRows) {
-          *reinterpret_cast<CV*>(out + xt.at(k, yy, kz)) = w[k];
-        } else if constexpr (SEG) {
-          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
-          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w[k];
-        } else {
-          at_byte(reinterpret_cast<CV*>(out), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
-                                               static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w[k];
-        }
-      }
-    }
-  };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
-  int tp = -1;  // tile whose output w holds
   for (; t < ntiles; t += G) {
     int f, y, kz0;
     decode(t, f, y, kz0);
-    lds_barrier();  // the previous tile's output has been read from s
+    lds_barrier();  // previous tile's stores have finished reading s
     // element (kx 0, kz 0) of field zero_mean_field reads as 0 (the omega_y source is the omega
     // state, whose mean line holds U(y)); it is kx row i = 0, the kz-0 column of each plane
     const bool zmean = !CMB && f == a.zero_mean_field && kz0 + a.kz_glob0 == 0;
@@ -567,7 +539,6 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
-    if (tp >= 0) store_out(tp);
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
@@ -581,10 +552,45 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           wave_fft<NX, RB, PITCH, true, TPR, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
-    read_out();
-    tp = t;
+    // output field of LDS column c (CMB: the group's two outputs) and its kz / plane
+    const int fa = CMB ? cmb_out_a(f) : f, fb = CMB ? cmb_out_b(f) : f;
+    T2* outa = phys + fa * a.field_stride_phys;
+    T2* outb = phys + fb * a.field_stride_phys;
+    if constexpr (kXRows) {
+#pragma unroll
+      for (int k = 0; k < KXS; ++k) {
+        const int e = tid + k * NT;
+        const int x = e / CWO, c = (e - x * CWO) * V;
+        const int cc = c % CL;
+        const int kz = kz0 + cc % KC, yy = y + cc / KC;
+        if (e < NX * CWO && kz < a.nkz && yy < a.ny) {
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          *reinterpret_cast<CV*>((c < CL ? outa : outb) + xt.at(k, yy, kz)) = w;
+        }
+      }
+      continue;
+    }
+    for (int e = tid; e < NX * CWO; e += NT) {
+      const int x = e / CWO, c = (e - x * CWO) * V;
+      const int cc = c % CL;
+      const int kz = kz0 + cc % KC, yy = y + cc / KC;
+      if (kz < a.nkz && yy < a.ny) {
+        CV w;
+#pragma unroll
+        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+        T2* out = c < CL ? outa : outb;
+        if constexpr (SEG) {
+          const SegPos sp = seg_find(a.x_start, a.poff, a.npseg, x);
+          *reinterpret_cast<CV*>(out + sp.off + (static_cast<long long>(yy) * sp.count + (x - sp.start)) * a.nkz + kz) = w;
+        } else {
+          at_byte(reinterpret_cast<CV*>(out), (static_cast<unsigned>(yy * NX + x) * static_cast<unsigned>(a.nkz) +
+                                               static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2))) = w;
+        }
+      }
+    }
   }
-  if (tp >= 0) store_out(tp);
 }
 
 template <int NX, typename T, bool SEG, int WIDE, int SM = kSegFull, int V = 1, int SL = 0>
@@ -619,8 +625,10 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
   constexpr int KE = (NKX * CW + NT - 1) / NT;  // store passes over the retained kx rows
   static_assert(SM != kSegRows || (NT % CW == 0 && KE <= kSegRowsMax), "row table: a thread's rows repeat per pass");
   SegRows<SM == kSegRows ? KE : 1> rt;
-  if constexpr (SM == kSegRows)
-    rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, seg_stride(a), tid);
+  if constexpr (SM == kSegRows) {
+    if (dst.rowtab) rt.template load_at<NKX>(dst.rowtab, a.seg_y0, tid / CW, NT / CW);
+    else rt.template build<NT, CW, NKX>(dst.kx_start, dst.off, dst.ndst, dst.self_seg, dst.nself, seg_stride(a), tid);
+  }
   // SEG (pencil: the x-expanded input blocked by x range) with row tables: the thread's x rows of
   // the fetch (x = (tid + q NT) / CW, clamped), looked up once
   constexpr bool kXRows = SEG && SM == kSegRows;
@@ -663,69 +671,12 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
       }
     }
   };
-  // deferred stores (as in xfft_backward_kernel): the retained kx rows of a tile go from LDS into
-  // registers after its FFT and out after the next tile is staged, ahead of its prefetch
-  static_assert(NT % CW == 0, "a thread's store column is the same for every access");
-  constexpr int DI = NT / CW;  // kx rows between a thread's store accesses
-  CV w[KE];
-  auto read_out = [&]() {
-    const int c = (tid % CW) * V;
-#pragma unroll
-    for (int k = 0; k < KE; ++k) {
-      const int i = min(tid / CW + k * DI, NKX - 1);
-      const int x = i <= KXH ? i : NX - (NKX - i);
-#pragma unroll
-      for (int u = 0; u < V; ++u) w[k].c[u] = s[(c + u) * PITCH + fft_pidx(x)];
-    }
-  };
-  auto store_out = [&](int tt) {
-    int f, y, kz0;
-    decode(tt, f, y, kz0);
-    const int c = (tid % CW) * V;
-    const int kz = kz0 + c % KC, yy = y + c / KC;
-    if (kz >= a.nkz || yy >= a.ny) return;
-    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
-    // this rank's own block goes straight into its spectral field (no self exchange)
-    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
-    unsigned Y = 0, KZ = 0;
-    if constexpr (SM == kSegRows) seg_yk(a.segblk, yy, kz, Y, KZ);
-    unsigned ot = 0;
-    if constexpr (SL && SM != kSegRows) ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
-    const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
-#pragma unroll
-    for (int k = 0; k < KE; ++k) {
-      const int i = tid / CW + k * DI;
-      if (!(KE * NT == NKX * CW || i < NKX)) continue;
-      if constexpr (SM == kSegRows) {
-        CV& r = *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ));
-        if (SL && a.nt) st_nt(r, w[k]);
-        else r = w[k];
-      } else if constexpr (SL) {
-        CV& r = at_byte(reinterpret_cast<CV*>(outb), ot + static_cast<unsigned>(i) * rs);
-        if (a.nt) st_nt(r, w[k]);
-        else r = w[k];
-      } else if constexpr (SM == kSegOne) {
-        CV& r = at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(yy * NKX + i) * static_cast<unsigned>(a.nkz) +
-                                                      static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
-        if (a.nt) st_nt(r, w[k]);
-        else r = w[k];
-      } else {
-        const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, k * DI, DI, i)
-                                        : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
-        T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
-        unsigned Ys, KZs;
-        seg_yk(a.segblk, yy, kz, Ys, KZs);
-        *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Ys) * sp.count + (i - sp.start)) * seg_stride(a) + KZs) = w[k];
-      }
-    }
-  };
   int t = static_cast<int>(xcd_remap(blockIdx.x, gridDim.x));
   if (t < ntiles) fetch(t);
-  int tp = -1;  // tile whose output w holds
   for (; t < ntiles; t += G) {
     int f, y, kz0;
     decode(t, f, y, kz0);
-    lds_barrier();  // the previous tile's output has been read from s
+    lds_barrier();
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -737,7 +688,6 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
     }
     lds_barrier();
     if (t + G < ntiles) fetch(t + G);
-    if (tp >= 0) store_out(tp);
     {
       constexpr int TPR = Cfg::TPR;
       constexpr int RW = C / (NT / TPR);  // rows (kz columns) owned by each wave (or wave pair)
@@ -751,10 +701,74 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           wave_fft<NX, RB, PITCH, false, TPR, false, true>(s + ((tid / TPR) * RW + rr) * PITCH, tws, tid % TPR);
     }
     lds_barrier();
-    read_out();
-    tp = t;
+    T2* outb = static_cast<T2*>(dst.base) + f * a.field_stride_spec;
+    if constexpr (SL && SM != kSegRows) {
+      // one column per thread (NT % CW == 0), kx rows one block-column stride apart
+      static_assert(NT % CW == 0, "a thread's column must be the same for every access");
+      const int c = (tid % CW) * V;
+      const int kz = kz0 + c % KC, yy = y + c / KC;
+      if (kz < a.nkz && yy < a.ny) {
+        const unsigned ot = spec_blk_off(a, yy, 0, kz) * static_cast<unsigned>(sizeof(T2));
+        const unsigned rs = static_cast<unsigned>(a.nkzs) * kSpecYBlock * static_cast<unsigned>(sizeof(T2));
+        CV* ov = reinterpret_cast<CV*>(outb);
+        for (int i = tid / CW; i < NKX; i += NT / CW) {
+          const int x = i <= KXH ? i : NX - (NKX - i);
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          if (a.nt) st_nt(at_byte(ov, ot + static_cast<unsigned>(i) * rs), w);
+          else at_byte(ov, ot + static_cast<unsigned>(i) * rs) = w;
+        }
+      }
+      continue;
+    }
+    // this rank's own block goes straight into its spectral field (no self exchange)
+    T2* soutb = dst.self_seg >= 0 ? static_cast<T2*>(dst.self_base) + f * dst.self_field_stride : outb;
+    if constexpr (SM == kSegRows) {
+#pragma unroll
+      for (int k = 0; k < KE; ++k) {
+        const int e = k * NT + tid;
+        const int i = e / CW, c = (e - i * CW) * V;
+        const int kz = kz0 + c % KC, yy = y + c / KC;
+        if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
+          const int x = i <= KXH ? i : NX - (NKX - i);
+          CV w;
+#pragma unroll
+          for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+          unsigned Y, KZ;
+          seg_yk(a.segblk, yy, kz, Y, KZ);
+          CV& r = *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ));
+          if (SL && a.nt) st_nt(r, w);
+          else r = w;
+        }
+      }
+      continue;
+    }
+    for (int e0 = 0; e0 < NKX * CW; e0 += NT) {
+      const int e = e0 + tid;
+      const int i = e / CW, c = (e - i * CW) * V;
+      const int kz = kz0 + c % KC, yy = y + c / KC;
+      if (e < NKX * CW && kz < a.nkz && yy < a.ny) {
+        const int x = i <= KXH ? i : NX - (NKX - i);
+        CV w;
+#pragma unroll
+        for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
+        if constexpr (SM == kSegOne) {
+          CV& r = at_byte(reinterpret_cast<CV*>(outb), (static_cast<unsigned>(y * NKX + i) * static_cast<unsigned>(a.nkz) +
+                                                        static_cast<unsigned>(kz)) * static_cast<unsigned>(sizeof(T2)));
+          if (a.nt) st_nt(r, w);
+          else r = w;
+        } else {
+          const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, e0 / CW, NT / CW, i)
+                                          : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
+          T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
+          unsigned Y, KZ;
+          seg_yk(a.segblk, y, kz, Y, KZ);
+          *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Y) * sp.count + (i - sp.start)) * seg_stride(a) + KZ) = w;
+        }
+      }
+    }
   }
-  if (tp >= 0) store_out(tp);
 }
 
 // The template arguments of the last x-transform launch of this thread, as in the rocprofv3 kernel
