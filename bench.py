@@ -107,6 +107,8 @@ def main() -> None:
     from channel_gpu_amd.parallel.native_bootstrap import init_native
     from channel_gpu_amd.utils.config import default_config
 
+    # (a torch import here would bind torch's bundled HIP runtime and RCCL before the native core)
+    assert "torch" not in sys.modules, "bench.py ranks must not import torch"
     if args.gpus > 1:
         # a first multi-GPU run must fail diagnosably, well inside the driver's time limit: the
         # communication watchdog raises on every rank after 120 s without progress (instead of a

@@ -89,7 +89,10 @@ void install_crash_handler() {
 int hip_runtime_version() {
   static const int v = [] {
     int r = 0;
-    (void)hipRuntimeGetVersion(&r);
+    if (hipRuntimeGetVersion(&r) != hipSuccess) {
+      (void)hipGetLastError();
+      r = 0;
+    }
     return r;
   }();
   return v;
@@ -125,6 +128,10 @@ Solver::Solver(const Config& cfg, int rank, int nranks, int device, const std::s
   fp64_ = cfg_.fp64();
   esz_ = fp64_ ? 16 : 8;
   HIP_CHECK(hipSetDevice(device_));
+  // cache the runtime version outside any stream capture: transforms_slab first asks for it inside
+  // a capture, where hipRuntimeGetVersion fails and left the cached value 0 (the two-compute-stream
+  // pipeline then silently stayed off in every captured step)
+  (void)hip_runtime_version();
   HIP_CHECK(hipStreamCreateWithFlags(&s_comp_, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&s_comm_, hipStreamNonBlocking));
   // A communicator exists for P > 1, and also at P = 1 when a unique id is passed: that runs the
@@ -311,12 +318,11 @@ void Solver::alloc() {
   ychunk_ = ystreams_ >= 2 ? std::max(2, planes_in(104)) : planes_in(144);  // (2048x633x2048: 2 planes, 300.8 vs 310.7 ms at 1)
   // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
   // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
-  // (several chunks keep the exchange pipelined); CHANNEL_PSTREAMS=2 alternates the chunks between
-  // two compute streams (opt-in: measured slower with a 1-rank RCCL communicator at the headline,
-  // 45.0 vs 43.1 ms/step with 6- vs 8-plane chunks, gpurun_out/g12_fc*.log), each then with the P = 1
-  // per-stream budget
+  // (several chunks keep the exchange pipelined); CHANNEL_PSTREAMS=2 runs each chunk's transforms
+  // as two parts on two compute streams (transforms_slab; the chunk budget is unchanged: the two
+  // parts together hold one chunk's intermediates)
   if (const char* ps = std::getenv("CHANNEL_PSTREAMS")) pstreams_ = std::max(1, std::min(2, std::atoi(ps)));
-  ychunk_p_ = std::min(64, pstreams_ >= 2 ? planes_in(104) : planes_in(144));
+  ychunk_p_ = std::min(64, planes_in(144));
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   // blocked layout at P > 1: exchange chunks of whole 8-plane tiles (contiguous blocks)
   if (comm_ && kzb_ && ychunk_p_ > 0) ychunk_p_ = std::max(kSpecYBlock, ychunk_p_ / kSpecYBlock * kSpecYBlock);
@@ -403,7 +409,7 @@ void Solver::free_all() {
   ev_comp2_ = nullptr;
   ev_join_.clear();
   s_extra_.clear();
-  for (auto* v : {&ev_cb_, &ev_cc_, &ev_kb_, &ev_fb_})
+  for (auto* v : {&ev_cb_, &ev_cc_, &ev_cc2_, &ev_kb_, &ev_fb_})
     for (auto e : *v) (void)hipEventDestroy(e);
   ev_kb_.clear();
   ev_fb_.clear();
@@ -418,6 +424,7 @@ void Solver::free_all() {
   tev_pool_.clear();
   ev_cb_.clear();
   ev_cc_.clear();
+  ev_cc2_.clear();
   step_ev_.clear();
   for (auto e : {ev_spec_, ev_phys_, ev_fwd_done_, ev_red_, ev_cfl_, ev_stats_, ev_tdt_[0], ev_tdt_[1], ev_dtf_[0], ev_dtf_[1]})
     if (e) (void)hipEventDestroy(e);
@@ -1238,9 +1245,10 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     HIP_CHECK(hipEventRecord(ev_cb_[k], s_comm_));
   };
   backward(0);
-  // chunks alternate between two compute streams (each chunk waits for its own backward exchange,
-  // which follows K-SPEC on the comm stream; chunks touch disjoint phys planes and exchange rows;
-  // the CFL maxima are atomic); phase timing keeps one stream so the stage times add up
+  // a chunk's transforms may run as two parts on two compute streams (below; each part waits for its
+  // chunk's backward exchange, which follows K-SPEC on the comm stream; parts touch disjoint phys
+  // planes and exchange rows; the CFL maxima are atomic); phase timing keeps one stream so the stage
+  // times add up
   // (not inside a stream capture on a HIP runtime older than 7.2: a process that imports torch
   // binds torch's bundled HIP 7.0 runtime and RCCL (same sonames), and there a captured step with the
   // second compute stream forked next to the RCCL exchanges segfaults in the runtime; eager steps and
@@ -1254,41 +1262,60 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   }();
   const bool two = s_comp2_ != nullptr && !phase_timing_ && nch > 1 &&
                    (cst == hipStreamCaptureStatusNone || hip_runtime_version() >= 70200000 || cap_force);
+  // two compute streams: each exchange chunk's transforms run as two parts of (about) half its rows,
+  // one per stream, both waiting for the chunk's backward exchange (the pair of parts in flight is
+  // one chunk's intermediates, as at P = 1, where alternating whole 8-plane chunks kept two chunks'
+  // intermediates in flight and overflowed the Infinity Cache); parts start on plane pairs (the
+  // plane tiles) and address their rows of the chunk's exchange blocks through XArgs::seg_yoff
+  while (static_cast<int>(ev_cc2_.size()) < nch) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev_cc2_.push_back(e);
+  }
+  if (markers_ && cst != hipStreamCaptureStatusNone && n == 0)
+    marker(two ? "capture: transforms on two compute streams" : "capture: transforms on one compute stream");
+  const int nparts = two ? 2 : 1;
+  const int part = nparts > 1 ? ((ch + 3) / 4) * 2 : ch;  // rows of the first part (even)
   for (int k = 0; k < nch; ++k) {
     if (k + 1 < nch) backward(k + 1);
-    hipStream_t cs = (two && (k & 1)) ? s_comp2_ : s_comp_;
-    HIP_CHECK(hipStreamWaitEvent(cs, ev_cb_[k], 0));
     const int y0 = k * ch, ny = std::max(0, std::min(ch, p.ny_loc - y0));
-    if (ny > 0) {
-      for (int c = 0; c < P; ++c)
-        for (int b = 0; b < NB; ++b)
-          src.off[c * NB + b] = dst.off[c * NB + b] =
-              (ny_pad * kb_gstart(c, b) + static_cast<long long>(y0) * kb_gcount(c, b)) * nkzs_;
-      if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields (block b)
-        for (int b = 0; b < NB; ++b)
-          src.off[p.rank * NB + b] = dst.off[p.rank * NB + b] =
-              static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * nkzs_;
-      XArgs xc = xa;
-      xc.ny = ny;
-      xc.nfields = 6;
-      xc.seg_y0 = kzb_ ? y0 / kSpecYBlock : y0;
-      char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0) * p.NX * p.nkz_loc * esz_;
-      ev(1, false, cs);
-      xfft_backward(xc, src, ph, tw_x_, fp64_, cs);
-      ev(1, true, cs);
-      ZArgs zc = za0;
-      zc.ny = ny;
-      zc.y0 = p.y0 + y0;
-      ev(2, false, cs);
-      zphys(zc, ph, tw_z_, fp64_, cs);
-      ev(2, true, cs);
-      xc.nfields = 3;
-      ev(3, false, cs);
-      xfft_forward(xc, ph, dst, tw_x_, fp64_, cs);
-      ev(3, true, cs);
+    for (int c = 0; c < P; ++c)
+      for (int b = 0; b < NB; ++b)
+        src.off[c * NB + b] = dst.off[c * NB + b] =
+            (ny_pad * kb_gstart(c, b) + static_cast<long long>(y0) * kb_gcount(c, b)) * nkzs_;
+    if (self_direct_)  // rows y0.. of this rank's y range in its own spectral fields (block b)
+      for (int b = 0; b < NB; ++b)
+        src.off[p.rank * NB + b] = dst.off[p.rank * NB + b] =
+            static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * nkzs_;
+    for (int h = 0; h < nparts; ++h) {
+      hipStream_t cs = h ? s_comp2_ : s_comp_;
+      HIP_CHECK(hipStreamWaitEvent(cs, ev_cb_[k], 0));
+      const int r0 = h ? std::min(part, ny) : 0;
+      const int nr = nparts > 1 ? (h ? ny - r0 : std::min(part, ny)) : ny;
+      if (nr > 0) {
+        XArgs xc = xa;
+        xc.ny = nr;
+        xc.nfields = 6;
+        xc.seg_y0 = kzb_ ? y0 / kSpecYBlock : y0;
+        xc.seg_yoff = r0;
+        char* ph = static_cast<char*>(phys_) + static_cast<size_t>(y0 + r0) * p.NX * p.nkz_loc * esz_;
+        ev(1, false, cs);
+        xfft_backward(xc, src, ph, tw_x_, fp64_, cs);
+        ev(1, true, cs);
+        ZArgs zc = za0;
+        zc.ny = nr;
+        zc.y0 = p.y0 + y0 + r0;
+        ev(2, false, cs);
+        zphys(zc, ph, tw_z_, fp64_, cs);
+        ev(2, true, cs);
+        xc.nfields = 3;
+        ev(3, false, cs);
+        xfft_forward(xc, ph, dst, tw_x_, fp64_, cs);
+        ev(3, true, cs);
+      }
+      HIP_CHECK(hipEventRecord(h ? ev_cc2_[k] : ev_cc_[k], cs));
+      HIP_CHECK(hipStreamWaitEvent(s_comm_, h ? ev_cc2_[k] : ev_cc_[k], 0));
     }
-    HIP_CHECK(hipEventRecord(ev_cc_[k], cs));
-    HIP_CHECK(hipStreamWaitEvent(s_comm_, ev_cc_[k], 0));
     if (fsplit && k == nch - 1) {
       // forward-path overlap: the CFL maxima first (every z stage is done), then the last chunk's
       // rows block by block; K-SPEC block b waits only for ev_fb_[b] (kspec())
@@ -1650,11 +1677,14 @@ void Solver::step(bool stats_for_next) {
         // A graph that is abandoned (here or after the cross-rank agreement below) must leave that
         // state as it was, or this rank's eager step would exchange other blocks than its peers'.
         presend_saved_ = presend_done_;
+        // (CHANNEL_MARKERS=1: one line per capture phase, to place a failure inside the runtime)
+        if (markers_) marker("capture: begin");
         HIP_CHECK(hipStreamBeginCapture(s_comp_, mode));
         try {
           capture_fail_test_ = inject;
           step_body(stats_for_next);
           capture_fail_test_ = false;
+          if (markers_) marker("capture: step recorded");
         } catch (...) {
           capture_fail_test_ = false;
           end_failed_capture();
@@ -1663,6 +1693,7 @@ void Solver::step(bool stats_for_next) {
           throw;
         }
         HIP_CHECK(hipStreamEndCapture(s_comp_, &g));
+        if (markers_) marker("capture: ended");
         // CHANNEL_GRAPH_DOT=<prefix>: the captured step graph as <prefix>_r<rank>_g<gi>.dot (topology
         // diagnosis: which nodes and cross-stream edges a replay has to honour)
         if (const char* dp = std::getenv("CHANNEL_GRAPH_DOT")) {
@@ -1670,6 +1701,7 @@ void Solver::step(bool stats_for_next) {
           if (hipGraphDebugDotPrint(g, path.c_str(), 0) != hipSuccess) (void)hipGetLastError();
         }
         HIP_CHECK(hipGraphInstantiate(&gexec_[gi], g, nullptr, nullptr, 0));
+        if (markers_) marker("capture: instantiated");
         (void)hipGraphDestroy(g);
       } catch (const Error& e) {
         std::cerr << "[channel] hipGraph capture failed, running eagerly: " << e.what() << "\n";
@@ -1711,6 +1743,7 @@ void Solver::step(bool stats_for_next) {
     }
     if (gexec_[gi]) {
       HIP_CHECK(hipGraphLaunch(gexec_[gi], s_comp_));
+      if (markers_ && !replayed_[gi]) marker("graph launched");
       done = true;
     }
   }

@@ -202,6 +202,8 @@ struct XArgs {
   // chunk rows start on 8-plane tiles).  fft_impl.hpp seg_yk / seg_stride
   int segblk = 0;
   int seg_y0 = 0;                    // with XSrc / XDst::rowtab: the chunk's first segment row Y
+  int seg_yoff = 0;                  // rows of the exchange chunk before this launch's first row (the
+                                     // second part of a chunk split over two compute streams)
   int nt = 0;                        // streaming (non-temporal) spectral accesses (solver default 1;
                                      // CHANNEL_XNT=0 off: 35.0 vs 34.75 ms/step, profiles/r04/ab_xnt.txt)
   // backward only: combine mode -- the six output fields u, v, w, omega_x, omega_y, omega_z are

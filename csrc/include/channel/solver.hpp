@@ -250,7 +250,7 @@ class Solver {
 
   std::vector<hipEvent_t> ev_a2a_, ev_xf_, ev_b_, ev_bb_;
   hipEvent_t ev_spec_ = nullptr, ev_phys_ = nullptr, ev_fwd_done_ = nullptr, ev_red_ = nullptr, ev_stats_ = nullptr;
-  std::vector<hipEvent_t> ev_cb_, ev_cc_;  // per y-chunk: backward exchange done, compute done
+  std::vector<hipEvent_t> ev_cb_, ev_cc_, ev_cc2_;  // per y-chunk: backward exchange done, compute done (part 0 / part 1)
   // pencil pipeline, per y chunk: A in, x-backward, B in, z stage, B out, x-forward done
   std::vector<hipEvent_t> ev_pen_[6];
   int ychunk_p_ = 0;                       // y planes per chunk of the P > 1 slab pipeline

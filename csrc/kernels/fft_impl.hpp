@@ -183,7 +183,8 @@ struct SegRows {
   __device__ __forceinline__ unsigned at(int k, unsigned Y, unsigned KZ) const { return a[k] + Y * b[k] + KZ; }
   __device__ __forceinline__ bool is_self(int k) const { return (self >> k) & 1u; }
 };
-// (Y, KZ) of element (y, kz) of an exchange segment or self block (offset = segment row base +
+// (Y, KZ) of element (y, kz) of an exchange segment or self block (y: the chunk's row plus
+// XArgs::seg_yoff, the first row of a part of an exchange chunk) (offset = segment row base +
 // Y * (rows stride) + KZ): plain [y][kx][kz] Y = y, KZ = kz; blocked (XArgs::segblk) Y = y / 8,
 // KZ = (y % 8) 8 + (kz / 8) 64 + kz % 8.  seg_stride: S of SegRows / the per-element lookups.
 __device__ __forceinline__ void seg_yk(int segblk, int y, int kz, unsigned& Y, unsigned& KZ) {
@@ -425,7 +426,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           // rows r0 + q DI from the row table (exchange segment or own block per row)
           const T2* sbase = in_self(f, k);
           unsigned Y, KZ;
-          seg_yk(1, min(y + c / KC, a.ny - 1), min(kz0 + c % KC, a.nkz - V), Y, KZ);
+          seg_yk(1, min(y + c / KC, a.ny - 1) + a.seg_yoff, min(kz0 + c % KC, a.nkz - V), Y, KZ);
 #pragma unroll
           for (int q = 0; q < EPT; ++q) {
             const CV& r = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, Y, KZ));
@@ -471,14 +472,14 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
           v[k][q] = a.nt ? ld_nt(r) : r;
         } else if constexpr (SM == kSegRows) {
           unsigned Y, KZ;
-          seg_yk(a.segblk, y, kz, Y, KZ);
+          seg_yk(a.segblk, y + a.seg_yoff, kz, Y, KZ);
           v[k][q] = *reinterpret_cast<const CV*>((rt.is_self(q) ? sbase : base) + rt.at(q, Y, KZ));
         } else {
           const SegPos sp = SM == kSegWin ? seg_find_win<kMaxSeg>(src.kx_start, src.off, src.nsrc, (q * NT) / CW, NT / CW, i)
                                           : seg_find<kMaxSeg>(src.kx_start, src.off, src.nsrc, i);
           const T2* b = static_cast<unsigned>(sp.idx - src.self_seg) < static_cast<unsigned>(src.nself) ? sbase : base;
           unsigned Y, KZ;
-          seg_yk(a.segblk, y, kz, Y, KZ);
+          seg_yk(a.segblk, y + a.seg_yoff, kz, Y, KZ);
           const long long S = seg_stride(a);
           // 32-bit offsets (checked on the host) keep the address in one VGPR: base in SGPRs
           v[k][q] = *reinterpret_cast<const CV*>(
@@ -736,7 +737,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
 #pragma unroll
           for (int u = 0; u < V; ++u) w.c[u] = s[(c + u) * PITCH + fft_pidx(x)];
           unsigned Y, KZ;
-          seg_yk(a.segblk, yy, kz, Y, KZ);
+          seg_yk(a.segblk, yy + a.seg_yoff, kz, Y, KZ);
           CV& r = *reinterpret_cast<CV*>((rt.is_self(k) ? soutb : outb) + rt.at(k, Y, KZ));
           if (SL && a.nt) st_nt(r, w);
           else r = w;
@@ -763,7 +764,7 @@ __global__ void __launch_bounds__((XCfg<NX, T, WIDE>::NT), (XCfg<NX, T, WIDE>::M
                                           : seg_find<kMaxSeg>(dst.kx_start, dst.off, dst.ndst, i);
           T2* ob = static_cast<unsigned>(sp.idx - dst.self_seg) < static_cast<unsigned>(dst.nself) ? soutb : outb;
           unsigned Y, KZ;
-          seg_yk(a.segblk, y, kz, Y, KZ);
+          seg_yk(a.segblk, y + a.seg_yoff, kz, Y, KZ);
           *reinterpret_cast<CV*>(ob + sp.off + (static_cast<long long>(Y) * sp.count + (i - sp.start)) * seg_stride(a) + KZ) = w;
         }
       }

@@ -86,3 +86,28 @@ def test_native_tcp_broadcast_missing_peer_times_out():
     env = dict(_tcp_env(0, 3, port), TMO="2")
     r = subprocess.run([sys.executable, "-c", _TCP_SCRIPT], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "peers connected" in r.stderr
+
+
+def test_rank_imports_stay_torch_free():
+    """bench.py's and the drivers' rank-side imports must not import torch: torch's bundled HIP
+    runtime and RCCL share /opt/rocm's sonames, and a torch import ahead of the native core binds the
+    solver to them (round 6: channel_gpu_amd.parallel imported its torch.distributed helpers eagerly,
+    so bench.py ran on torch's HIP 7.0 runtime, where captured steps keep one compute stream)."""
+    import subprocess
+    import sys
+
+    code = (
+        "import os, sys\n"
+        "os.environ['CHANNEL_TORCH_FREE'] = '1'\n"
+        "from channel_gpu_amd import require_core\n"
+        "from channel_gpu_amd.parallel.decomposition import PencilDecomposition, SlabDecomposition\n"
+        "from channel_gpu_amd.parallel.native_bootstrap import init_native\n"
+        "from channel_gpu_amd.utils.config import default_config\n"
+        "import channel_gpu_amd.driver\n"
+        "assert 'torch' not in sys.modules, sorted(m for m in sys.modules if m.startswith('torch'))[:5]\n"
+        "from channel_gpu_amd.parallel import dist_info  # the lazy torch.distributed helpers still resolve\n"
+        "print('TORCH_FREE_OK')\n"
+    )
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=__import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+    assert r.returncode == 0 and "TORCH_FREE_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

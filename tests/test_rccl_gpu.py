@@ -258,7 +258,7 @@ def test_rccl_two_compute_streams_bitwise(native, monkeypatch):
 
 
 PSTREAMS_SCRIPT = r"""
-import os, sys
+import json, os, sys
 import numpy as np
 sys.path.insert(0, os.environ["CHANNEL_ROOT"])
 from channel_gpu_amd import require_core
@@ -266,6 +266,7 @@ from channel_gpu_amd.utils.config import default_config
 C = require_core()
 kw = dict(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
           log_every=0, symmetry_every=0)
+kw.update(json.loads(os.environ.get("PSTREAMS_KW", "{}")))
 out = []
 for uid in (b"", C.new_unique_id()):
     s = C.Solver(default_config(**kw), 0, 1, 0, uid)
@@ -280,15 +281,23 @@ print("PSTREAMS_OK", flush=True)
 """
 
 
-def test_rccl_two_compute_streams_captured_torch_free(native):
+@pytest.mark.parametrize("layout", ["plain", "blocked"])
+def test_rccl_two_compute_streams_captured_torch_free(native, layout):
     """CHANNEL_PSTREAMS=2 inside the captured step graph, in a torch-free process (ROCm 7.2's
-    runtime and RCCL, like bench.py and the drivers), bitwise the fast path."""
+    runtime and RCCL, like bench.py and the drivers), bitwise the fast path.  Each exchange chunk's
+    transforms run as two parts, one per compute stream (XArgs::seg_yoff): plain [y][line] layout
+    with 16-plane chunks, and the blocked layout's plane tiles (NX = 512 fp32, 8-plane chunks split
+    4 + 4 inside the 8-plane tiles)."""
+    import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, CHANNEL_TORCH_FREE="1", CHANNEL_PSTREAMS="2", CHANNEL_YCHUNK="16", CHANNEL_ROOT=root)
+    if layout == "blocked":
+        env.update(CHANNEL_SPEC_KZB="1", CHANNEL_YCHUNK="8", CHANNEL_COMBINE="1",
+                   PSTREAMS_KW=json.dumps(dict(NX=512, NY=65, NZ=129, precision="fp32", Re=2000.0)))
     r = subprocess.run([sys.executable, "-c", PSTREAMS_SCRIPT], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "PSTREAMS_OK" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-3000:])
 

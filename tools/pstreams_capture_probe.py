@@ -5,7 +5,9 @@ P > 1 step graph with the second compute stream forked next to the RCCL exchange
 RCCL communicator.  Prints which HIP runtime the process bound and, on a crash, the native
 backtrace (install_crash_handler).
 
-  CHANNEL_PSTREAMS=2 CHANNEL_PSTREAMS_CAPTURE=1 python tools/pstreams_capture_probe.py [--torch-free]
+  CHANNEL_PSTREAMS=2 CHANNEL_PSTREAMS_CAPTURE=1 CHANNEL_MARKERS=1 python tools/pstreams_capture_probe.py [--torch-free]
+(CHANNEL_MARKERS=1: the solver's stderr markers around the capture, instantiation and first replay;
+CHANNEL_GRAPH_DOT=<prefix>: the captured step graph's topology, where the capture completes)
 """
 import ctypes
 import os
@@ -29,6 +31,7 @@ os.environ.setdefault("CHANNEL_YCHUNK", "8")
 cfg = default_config(NX=64, NY=65, NZ=33, Re=1000.0, precision="fp64", ic="random", ic_amplitude=0.2, stats_every=0,
                      log_every=0, symmetry_every=0)
 s = C.Solver(cfg, 0, 1, 0, C.new_unique_id())
+C.install_crash_handler()  # again: RCCL's communicator setup may install its own SIGSEGV handler
 s.init_ic()
 s.prepare()
 for i in range(4):
