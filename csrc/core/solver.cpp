@@ -182,10 +182,14 @@ void Solver::choose_layout() {
   const Plan& p = plan_;
   // The physical-stage fields: at P > 1 K-SPEC writes D1 v, v, D1 omega and the x-backward forms
   // u, w, omega_x, omega_z from them (combine): the backward exchange moves 5 fields instead of 6.
-  // At one rank (no exchange, also the 1-rank RCCL communicator) K-SPEC writes the six fields: the
-  // same K-SPEC time (4.15 ms per substep with 7 or 9 stores) and one-input x-backward tiles of
-  // whole 128-B lines, 61 vs 71 us per 6-plane chunk (profiles/r06/).  CHANNEL_COMBINE=0/1 forces it.
-  combine_ = comm_ && p.P > 1;
+  // At one rank (no exchange, also the 1-rank RCCL communicator) K-SPEC writes the six fields (the
+  // combine mode measured the same there, 32.54 vs 32.53 ms/step: K-SPEC takes the same time with 7
+  // or 9 stores; profiles/r06/ab_start_combine_forcecomm.txt).  Where the exchange sets the pace
+  // (the busiest-link model of BASELINE.md §3: P = 2 and 4 at the headline, exchange >= compute) one
+  // sixth fewer backward bytes pay for the combine mode's two-input x-backward tiles (34.98 vs 33.78
+  // ms/step of per-rank work at the headline on one GPU); at P >= 5 the step is compute-bound and
+  // the six-output mode stays.  CHANNEL_COMBINE=0/1 forces either.
+  combine_ = comm_ && p.P > 1 && p.P <= 4;
   if (const char* e = std::getenv("CHANNEL_COMBINE")) combine_ = std::atoi(e) != 0;
   kzb_ = (p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = std::atoi(e) != 0 ? kSpecKzBlock : 0;
@@ -318,9 +322,11 @@ void Solver::alloc() {
   ychunk_ = ystreams_ >= 2 ? std::max(2, planes_in(104)) : planes_in(144);  // (2048x633x2048: 2 planes, 300.8 vs 310.7 ms at 1)
   // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
   // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
-  // (several chunks keep the exchange pipelined); CHANNEL_PSTREAMS=2 runs each chunk's transforms
-  // as two parts on two compute streams (transforms_slab; the chunk budget is unchanged: the two
-  // parts together hold one chunk's intermediates)
+  // (several chunks keep the exchange pipelined); each chunk's transforms run as two parts on two
+  // compute streams (transforms_slab; the chunk budget is unchanged: the two parts together hold one
+  // chunk's intermediates): with a 1-rank RCCL communicator 35.9 -> 33.8 ms/step against the 31.9
+  // fast path (profiles/r06/ab_p_gt_1_plane_tiles.txt); CHANNEL_PSTREAMS=1 keeps one stream
+  pstreams_ = 2;
   if (const char* ps = std::getenv("CHANNEL_PSTREAMS")) pstreams_ = std::max(1, std::min(2, std::atoi(ps)));
   ychunk_p_ = std::min(64, planes_in(144));
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);

@@ -10,9 +10,11 @@
 //   (convolution.c:7-20, convolution_kernels.cu:7-66), calcSt plane sums (statistics.cu:7-95).
 // The reference runs these as ~50 launches + 44 cusparse calls + 8 D2D copies per substep with
 // float<->double casts through HBM.  Here one launch reads 7 fields (5 on the first substep) and
-// writes 7 (5 on the last: R_phi, R_omega are not needed there): the states phi and omega, R_phi,
-// R_omega, and v, D1 v, D1 omega, from which the x-backward forms the six fields of the
-// physical-space stage (XArgs::combine).  All y-work is fp64 in registers, and the wall-normal
+// writes the states phi and omega, R_phi and R_omega (not on the last substep: the next one has
+// zeta = 0) and the physical-stage inputs: u, v, w, omega_x, omega_z (the six-output mode, one
+// rank and P >= 5: 9 stores, 7 on the last substep; the omega state is the omega_y field) or v,
+// D1 v, D1 omega, from which the x-backward forms the six fields (XArgs::combine, P = 2..4: 7
+// stores, 5 on the last substep).  All y-work is fp64 in registers, and the wall-normal
 // operators are applied in "M-form" (the compact D2 mass matrix multiplies the equation), so the
 // explicit viscous term needs no solve at all.
 //

@@ -177,6 +177,11 @@ def test_eight_ranks_uneven_realistic_shape(native, monkeypatch, pr):
     grid = dict(NX=64, NY=385, NZ=33)
     monkeypatch.setenv("CHANNEL_YCHUNK", "16")
     monkeypatch.setenv("CHANNEL_SHM_SLOT_MB", "8")
+    # the slab runs the combine mode (the P <= 4 default, forced here), the pencil the six-output
+    # mode (the default at 8 ranks); the single-rank reference runs the same mode (spawned ranks
+    # inherit the environment at spawn)
+    combine = "1" if pr == 1 else "0"
+    monkeypatch.setenv("CHANNEL_COMBINE", combine)
     world, nsteps = 8, 2
     shm = f"shm:chtest8_{uuid.uuid4().hex[:12]}"
     with tempfile.TemporaryDirectory() as d:
@@ -187,11 +192,10 @@ def test_eight_ranks_uneven_realistic_shape(native, monkeypatch, pr):
 
     cfg = default_config(**grid, Re=2000.0, precision="fp64", ic="random", ic_amplitude=0.05, stats_every=0,
                          log_every=0, symmetry_every=0)
-    # the single-rank reference in the combine mode of P > 1 (K-SPEC's D1 v / v / D1 omega outputs,
+    # the single-rank reference in the ranks' mode (combine: K-SPEC's D1 v / v / D1 omega outputs,
     # the combining x-backward), the arithmetic the 8 ranks run
-    monkeypatch.setenv("CHANNEL_COMBINE", "1")
     s1 = native.Solver(cfg, 0, 1, 0, b"")
-    assert s1.combine()
+    assert s1.combine() == (combine == "1")
     s1.init_ic()
     s1.prepare()
     for _ in range(nsteps):
