@@ -190,6 +190,7 @@ PYBIND11_MODULE(_core, m) {
       .def("stats", [](Solver& s) { return vec(s.stats()); })
       .def("kblocks", &Solver::kblocks)
       .def("bwd_blocks_issued", &Solver::bwd_blocks_issued)
+      .def("captured_compute_streams", &Solver::captured_compute_streams)
       .def("spec_kzb", &Solver::spec_kzb)
       .def("combine", &Solver::combine)
       .def("mean_profile", [](Solver& s) { return vec(s.mean_profile()); })

@@ -1278,6 +1278,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
     HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     ev_cc2_.push_back(e);
   }
+  if (cst != hipStreamCaptureStatusNone) captured_streams_ = two ? 2 : 1;
   if (markers_ && cst != hipStreamCaptureStatusNone && n == 0)
     marker(two ? "capture: transforms on two compute streams" : "capture: transforms on one compute stream");
   const int nparts = two ? 2 : 1;

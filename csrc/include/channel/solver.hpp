@@ -140,6 +140,8 @@ class Solver {
   // backward-exchange kx sub-block groups issued so far (host count: the pipeline bookkeeping of
   // the pre-send, checked by the capture-failure test)
   long long bwd_blocks_issued() const { return bwd_blocks_issued_; }
+  // compute streams of the last P > 1 transform stage recorded inside a stream capture (0: none yet)
+  int captured_compute_streams() const { return captured_streams_; }
   int spec_kzb() const { return kzb_; }  // spectral layout (spec_index)
   // abort every communicator (the per-axis split ones first: aborting the parent does not abort
   // communicators split from it), so no stream stays blocked in an exchange with a dead peer
@@ -272,6 +274,7 @@ class Solver {
   bool presend_done_ = false;
   bool presend_saved_ = false;  // presend_done_ before a step capture (restored if the graph is dropped)
   long long bwd_blocks_issued_ = 0;
+  int captured_streams_ = 0;
   int xnt_ = 0;  // non-temporal spectral accesses in the x transforms (XArgs::nt)
   bool kb_overlap() const { return nkb_ > 1 && comm_ != nullptr; }
   // Forward-path overlap (slab, kx sub-blocks): the last y chunk's forward exchange goes out block
