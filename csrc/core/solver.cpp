@@ -323,12 +323,15 @@ void Solver::alloc() {
   // P > 1 slab: ~144 MiB per chunk; each chunk is also one batched exchange per direction, so the
   // exchange of chunk k+1 (and the return of chunk k-1) overlaps the transforms of chunk k
   // (several chunks keep the exchange pipelined); each chunk's transforms run as two parts on two
-  // compute streams (transforms_slab; the chunk budget is unchanged: the two parts together hold one
-  // chunk's intermediates): with a 1-rank RCCL communicator 35.9 -> 33.8 ms/step against the 31.9
-  // fast path (profiles/r06/ab_p_gt_1_plane_tiles.txt); CHANNEL_PSTREAMS=1 keeps one stream
+  // compute streams (transforms_slab), each part with the one-stream chunk's budget (~144 MiB: 8
+  // planes at the headline): with a 1-rank RCCL communicator 35.9 (one stream, 8-plane chunks) ->
+  // 34.2 (4 + 4-plane parts) -> 33.4 ms/step (8 + 8) against the 32.0 fast path; the 4-plane parts'
+  // kernels ran mostly partial rounds of tiles (x-forward: 258 tiles for 256 CUs).  At slab8 (48-49
+  // planes per rank) that is 4 chunks, and the exchange of a chunk's last kx sub-block is ~0.1 ms
+  // (profiles/r06/ab_p_gt_1_plane_tiles.txt).  CHANNEL_PSTREAMS=1 keeps one stream
   pstreams_ = 2;
   if (const char* ps = std::getenv("CHANNEL_PSTREAMS")) pstreams_ = std::max(1, std::min(2, std::atoi(ps)));
-  ychunk_p_ = std::min(64, planes_in(144));
+  ychunk_p_ = std::min(64, planes_in(pstreams_ >= 2 && !plan_.pencil() ? 288 : 144));  // (the pencil: one stream)
   if (const char* yc = std::getenv("CHANNEL_YCHUNK")) ychunk_ = ychunk_p_ = std::atoi(yc);
   // blocked layout at P > 1: exchange chunks of whole 8-plane tiles (contiguous blocks)
   if (comm_ && kzb_ && ychunk_p_ > 0) ychunk_p_ = std::max(kSpecYBlock, ychunk_p_ / kSpecYBlock * kSpecYBlock);
@@ -1281,7 +1284,12 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
   if (cst != hipStreamCaptureStatusNone) captured_streams_ = two ? 2 : 1;
   if (markers_ && cst != hipStreamCaptureStatusNone && n == 0)
     marker(two ? "capture: transforms on two compute streams" : "capture: transforms on one compute stream");
-  const int nparts = two ? 2 : 1;
+  // CHANNEL_PSPLIT=0: whole chunks alternate between the two streams instead (A/B)
+  static const bool psplit = [] {
+    const char* e = std::getenv("CHANNEL_PSPLIT");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const int nparts = two && psplit ? 2 : 1;
   const int part = nparts > 1 ? ((ch + 3) / 4) * 2 : ch;  // rows of the first part (even)
   for (int k = 0; k < nch; ++k) {
     if (k + 1 < nch) backward(k + 1);
@@ -1295,7 +1303,7 @@ void Solver::transforms_slab(int n, const XArgs& xa0, const ZArgs& za0, const Dt
         src.off[p.rank * NB + b] = dst.off[p.rank * NB + b] =
             static_cast<long long>(kb_off_[b]) + (static_cast<long long>(p.y0) + y0) * kb_cnt_[b] * nkzs_;
     for (int h = 0; h < nparts; ++h) {
-      hipStream_t cs = h ? s_comp2_ : s_comp_;
+      hipStream_t cs = (h || (two && !psplit && (k & 1))) ? s_comp2_ : s_comp_;
       HIP_CHECK(hipStreamWaitEvent(cs, ev_cb_[k], 0));
       const int r0 = h ? std::min(part, ny) : 0;
       const int nr = nparts > 1 ? (h ? ny - r0 : std::min(part, ny)) : ny;
