@@ -191,6 +191,15 @@ void Solver::choose_layout() {
   // the six-output mode stays.  CHANNEL_COMBINE=0/1 forces either.
   combine_ = comm_ && p.P > 1 && p.P <= 4;
   if (const char* e = std::getenv("CHANNEL_COMBINE")) combine_ = std::atoi(e) != 0;
+  {
+    // fp64 storage from R = 10: K-SPEC is built for the six-output mode only (kspec_impl.hpp kSixOnly)
+    int R = 1, H = 1;
+    kspec_geometry(cfg_.NY, fp64_, R, H);
+    if (combine_ && fp64_ && R >= 10) {
+      if (std::getenv("CHANNEL_COMBINE")) std::fprintf(stderr, "[channel] CHANNEL_COMBINE ignored: fp64 at R >= 10 runs the six-output mode\n");
+      combine_ = false;
+    }
+  }
   kzb_ = (p.R >= 7 && p.R <= 8) ? kSpecKzBlock : 0;
   if (const char* e = std::getenv("CHANNEL_SPEC_KZB")) kzb_ = std::atoi(e) != 0 ? kSpecKzBlock : 0;
   // (the x transforms address a blocked field with 32-bit byte offsets: above 4 GiB per field the

@@ -388,6 +388,11 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
   constexpr int ROWS = 64 * R * H;  // rows of a line (table stride)
   constexpr int NT = W * 64 * H;
   constexpr int NF = PFac<R>::kNumFields;
+  // fp64 storage from R = 10 runs the six-output mode only (the solver never selects the combine
+  // mode there): without the combine branch the register allocation of these spill-prone kernels
+  // does not have to cover both output stages
+  constexpr bool kSixOnly = sizeof(T) == 8 && R >= 10;
+  const bool out6 = kSixOnly || a.out6;
   constexpr bool TLDS = kspec_tables_in_lds<R, T, W, H>();
   constexpr int NTAB = kspec_lds_tables_doubles<R, T, W, H>();
   constexpr bool kDoubleTile = kspec_double_tile<R, T, W, H>();
@@ -883,7 +888,7 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
         }
       }
       // (STORE2 with the combine outputs: phi goes out at the end, paired with D1 omega)
-      if (!kStore2 || a.out6) st.store(phi, ph);
+      if (!kStore2 || out6) st.store(phi, ph);
       KSPEC_STAMP(6)
       // the next tile's first inputs load during the D1 solve and the output stores (the async
       // LDS copies go out after the output stores instead: those use both tiles)
@@ -997,11 +1002,11 @@ __global__ void __launch_bounds__(W * 64 * H) kspec_kernel(YTab tg, SpecArgs a) 
     // operator) omega_x = Dw - i be v = i (be phi + al D1 omega)/k2 and omega_z = i al v - Du =
     // i (be D1 omega - al phi)/k2 (convolution_kernels.cu:46-53; mean line: u = U, omega_z = -dU/dy).
     // Three field stores instead of five per substep, and the exchange of P > 1 moves five fields.
-    if (a.out6) {
+    if (out6) {
       // The six physical-stage fields themselves (u, v, w, omega_x, omega_z; omega_y is the omega
-      // state): at one rank the x-backward then reads one field per tile (two planes of a kz block,
-      // whole 128-B lines) -- 61 vs 71 us per 6-plane chunk for the combine mode's two-input tiles,
-      // while K-SPEC takes the same 4.15 ms per substep with 9 or 7 stores (profiles/r06/)
+      // state): the x-backward then reads one field per tile (two planes of a kz block, whole 128-B
+      // lines), while K-SPEC takes the same time with 9 or 7 stores (32.53 vs 32.54 ms/step at one
+      // rank: profiles/r06/ab_start_combine_forcecomm.txt, kspec_write_size_combine.txt)
       // wx = Dw - i be v = i (be phi + al D1 omega)/k2 - (v terms that cancel), written as in the
       // reference's calcOmega with D(dv) = D2 v = phi + k2 v (convolution_kernels.cu:46-53)
       auto omx = [&](int r, double& re, double& im) {
